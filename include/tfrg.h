@@ -1,0 +1,136 @@
+/* tfrg.h — C-ABI of libtfrg, the MI355X TFRecord -> tf.train.Example -> Feature decode path.
+ *
+ * Plain pointers and sizes only (no torch / HIP types): the Python host mirror binds it with
+ * ctypes (which releases the GIL), see INTEGRATION.md for the binding stubs. Every entry point
+ * cites the reference interface (kmkolasinski/tfrecords-reader v1.1.0) whose work it replaces.
+ *
+ * Return convention: int functions return 0 on success and a negative TFRG_E_* code on a runtime
+ * failure (HIP error, bad argument, allocation). Per-record DATA errors are never return codes:
+ * they are the per-record int32 status column (include/tfrg_status.h), mirroring the exception the
+ * reference would raise for that record.
+ */
+#ifndef TFRG_H
+#define TFRG_H
+#include <stdint.h>
+#include "tfrg_status.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFRG_ABI_VERSION 1
+
+/* runtime error codes (return values) */
+#define TFRG_E_ARG (-1)
+#define TFRG_E_HIP (-2)
+#define TFRG_E_NOMEM (-3)
+#define TFRG_E_IO (-4)
+#define TFRG_E_LIMIT (-5)
+
+/* decode flags */
+#define TFRG_FLAG_PAYLOAD_ONLY 1u /* ranges are bare Example payloads (decode(raw) semantics)   */
+#define TFRG_FLAG_SPEC_VARINT 2u  /* protobuf-spec int64 varints instead of the reference's
+                                     int-width shift (decoder.pyx:44)               */
+#define TFRG_FLAG_NO_CRC 4u       /* skip the CRC-32C verdicts                                   */
+
+int tfrg_abi_version(void);
+/* message of the last runtime failure on this thread */
+const char* tfrg_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------
+ * Host framing index (replaces cython/indexer.pyx:212-252 create_tfrecord_pointers_index).
+ * Pointers are (start, end, example_size) u64 triples, end = start + 16 + size; bit-exact with the
+ * reference, including its acceptance of a last record that runs past EOF.
+ * ------------------------------------------------------------------------------------------- */
+/* over an in-memory file image; writes up to cap triples, returns the record count */
+int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out_triples, int64_t cap);
+/* mmap + index; *out_triples is malloc'd (free with tfrg_free) */
+int tfrg_index_file(const char* path, uint64_t** out_triples, int64_t* n);
+/* .idx cache file, indexer.pyx:260-328: native size_t n, then n x {u64 start, end, size} */
+int tfrg_idx_save(const char* idx_path, const uint64_t* triples, int64_t n);
+int tfrg_idx_load(const char* idx_path, uint64_t** out_triples, int64_t* n);
+void tfrg_free(void* p);
+
+/* CRC-32C (Castagnoli) and the TFRecord mask (absent from the reference) */
+uint32_t tfrg_crc32c(const uint8_t* p, uint64_t n);
+uint32_t tfrg_masked_crc32c(const uint8_t* p, uint64_t n);
+/* TFRecord writer framing: n payloads (concatenated, offsets[n+1]) -> framed bytes with spec CRCs
+ * (crc != 0) or the zero CRCs the reference's test writers use (tests/utils.py:31-36).
+ * Returns the framed size; writes only if out_cap suffices. */
+int64_t tfrg_frame_records(const uint8_t* payloads, const uint64_t* offsets, int64_t n, int crc,
+                           uint8_t* out, int64_t out_cap);
+
+/* ---------------------------------------------------------------------------------------------
+ * Device decode (replaces cython/decoder.pyx:107 example_from_bytes per record, batched).
+ * One context per (device, host thread); calls on one context are serialised by the caller.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct tfrg_ctx tfrg_ctx;
+
+int tfrg_ctx_create(int device, tfrg_ctx** out);
+int tfrg_ctx_destroy(tfrg_ctx* ctx);
+/* records larger than lane_max bytes take the wavefront-per-record kernels (default 16384) */
+int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
+
+/* Key table ("schema"): n_keys distinct key byte strings (key_blob[key_offsets[i]..[i+1]]),
+ * key_flags bit0 = the bytes are not valid UTF-8 (decoder.pyx:164 would raise); n_slots columns,
+ * slot s = (slot_key[s], slot_kind[s]) with kind 1 bytes_list, 2 float_list, 3 int64_list.
+ * Records whose keys are not all in the table finish with status TFRG_ST_SCHEMA_MISS and list the
+ * missing (key, kind) pairs (tfrg_result_misses): intern them and decode again. */
+int tfrg_set_schema(tfrg_ctx* ctx, uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
+                    const uint32_t* key_flags, uint32_t n_slots, const uint32_t* slot_key,
+                    const uint8_t* slot_kind);
+
+/* Asynchronous decode of n records [start[i], end[i]) of a device buffer (framed TFRecords unless
+ * TFRG_FLAG_PAYLOAD_ONLY). d_bytes must stay readable up to round_up(nbytes, 16) and nbytes must be
+ * < 2^32 (split larger batches). d_start/d_end are device arrays. stream: hipStream_t or NULL for
+ * the context's own stream. Results stay valid until the next decode on this context. */
+int tfrg_decode_device(tfrg_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_start,
+                       const uint64_t* d_end, uint32_t n, uint32_t flags, void* stream);
+/* Same from host memory: stages bytes/start/end into context-owned HBM (H2D on the stream). */
+int tfrg_decode_host(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                     const uint64_t* h_end, uint32_t n, uint32_t flags, void* stream);
+
+typedef struct tfrg_info {
+  uint32_t n_records;
+  uint32_t n_slots;
+  uint32_t n_errors;        /* records whose status is a decode error           */
+  uint32_t first_error;     /* lowest such record index, 0xffffffff if none      */
+  uint32_t n_miss_records;  /* records with TFRG_ST_SCHEMA_MISS                   */
+  uint32_t n_miss_entries;  /* missing (key, kind) entries reported (may exceed the list capacity) */
+  uint32_t n_big;           /* records decoded by the wavefront-per-record kernels */
+  uint32_t scan_timeout;    /* must be 0                                          */
+  uint64_t kind_totals[4];  /* values per kind: [1] bytes elements, [2] floats, [3] int64s */
+  uint64_t nbytes;
+} tfrg_info;
+
+/* Waits for the last decode and returns its summary. */
+int tfrg_result_info(tfrg_ctx* ctx, tfrg_info* info);
+
+/* Columnar result. Per record: status/aux/verdict. Per slot s (row-major [n_slots][n]):
+ * order (0 absent, else 1 + the key's position in the record's dict), row_splits [n_slots][n+1]
+ * (element offsets inside the slot's column), slot_base [n_slots] (column start inside its kind's
+ * value array). Values: int64, float bits, bytes views (absolute offset into the input buffer,
+ * length). miss: [min(n_miss_entries, cap)][4] = (record, kind, key offset, key length). */
+typedef struct tfrg_columns {
+  int32_t* status;
+  int64_t* aux;
+  uint8_t* verdict;
+  uint16_t* order;
+  uint32_t* row_splits;
+  uint64_t* slot_base;
+  int64_t* i64;
+  uint32_t* f32;
+  uint32_t* bytes_off;
+  uint32_t* bytes_len;
+  uint32_t* miss;
+} tfrg_columns;
+
+/* device pointers of the last result (valid until the next decode / destroy) */
+int tfrg_result_device(tfrg_ctx* ctx, tfrg_columns* cols);
+/* copy the last result into caller host buffers sized from tfrg_info; NULL members are skipped */
+int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,398 @@
+// tfrg_capi.cpp — device context of libtfrg: key table upload, HBM arena, decode orchestration and
+// result transfer (include/tfrg.h). The kernels live in tfrg_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/tfrg.h"
+#include "crc32c.h"
+#include "tfrg_internal.h"
+
+namespace tfrg {
+void set_error(const std::string& s);
+
+#define HIP_TRY(expr)                                                              \
+  do {                                                                             \
+    hipError_t e_ = (expr);                                                        \
+    if (e_ != hipSuccess) {                                                        \
+      set_error(std::string(#expr) + ": " + hipGetErrorString(e_));               \
+      return TFRG_E_HIP;                                                           \
+    }                                                                              \
+  } while (0)
+
+// grow-only device buffer
+struct DBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= cap && p) return hipSuccess;
+    if (p) {
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      cap = 0;
+    }
+    size_t want = bytes < 256 ? 256 : bytes;
+    want = (want + 4095) & ~(size_t)4095;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) cap = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return reinterpret_cast<T*>(p);
+  }
+};
+
+constexpr uint32_t kMissCap = 1u << 16;
+
+}  // namespace tfrg
+
+using namespace tfrg;
+
+struct tfrg_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t last_stream = nullptr;
+  uint32_t lane_max = 16384;
+  int num_cus = 256;
+  // constants
+  DBuf crc_tab, consts;
+  // schema
+  DBuf ht, key_hash, key_off, key_blob, key_slot, slot_kind;
+  uint32_t n_keys = 0, n_slots = 0, ht_mask = 0;
+  // host staging for tfrg_decode_host
+  DBuf in_bytes, in_start, in_end;
+  // arena
+  DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
+  DBuf i64, f32, b_off, b_len, big_list, miss, info, granules, ticket;
+  // last batch
+  uint32_t n = 0;
+  uint64_t nbytes = 0;
+  uint64_t cap_i64 = 0, cap_f32 = 0, cap_b = 0;
+  bool have_result = false;
+};
+
+extern "C" {
+
+int tfrg_ctx_create(int device, tfrg_ctx** out) {
+  *out = nullptr;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) {
+    set_error("bad device index");
+    return TFRG_E_ARG;
+  }
+  HIP_TRY(hipSetDevice(device));
+  tfrg_ctx* c = new tfrg_ctx();
+  c->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    set_error("hipStreamCreate failed");
+    return TFRG_E_HIP;
+  }
+  // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192; consts: 64 lane shifts x^(128 l)
+  // and 16 un-shifts x^(-8z)
+  std::vector<uint32_t> tab(2048), cst(80);
+  CrcTables T;
+  crc_make_tables(&T);
+  memcpy(tab.data(), T.t, 4096);
+  uint32_t M[4][256];
+  crc_make_mul_tables(gf_xpow8(1024), M);
+  memcpy(tab.data() + 1024, M, 4096);
+  for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
+  for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
+  if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||
+      hipMemcpy(c->crc_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(c->consts.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    set_error("constant upload failed");
+    tfrg_ctx_destroy(c);
+    return TFRG_E_HIP;
+  }
+  *out = c;
+  return 0;
+}
+
+int tfrg_ctx_destroy(tfrg_ctx* c) {
+  if (!c) return 0;
+  (void)hipSetDevice(c->device);
+  if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
+  DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
+                 &c->slot_kind, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
+                 &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
+                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->granules, &c->ticket};
+  for (DBuf* b : all) b->release();
+  if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  delete c;
+  return 0;
+}
+
+int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
+  if (!c) return TFRG_E_ARG;
+  c->lane_max = lane_max;
+  return 0;
+}
+
+static uint32_t fnv1a(const uint8_t* p, uint64_t n) {
+  uint32_t h = 2166136261u;
+  for (uint64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 16777619u;
+  return h;
+}
+
+int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
+                    const uint32_t* key_flags, uint32_t n_slots, const uint32_t* slot_key, const uint8_t* slot_kind) {
+  if (!c) return TFRG_E_ARG;
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  uint32_t hsz = 16;
+  while (hsz < 2 * n_keys + 2) hsz <<= 1;
+  std::vector<uint32_t> ht(hsz, 0), hash(n_keys ? n_keys : 1), off(n_keys + 1);
+  std::vector<int32_t> ks(4ull * (n_keys ? n_keys : 1), -1);
+  const uint64_t blob_len = n_keys ? key_offsets[n_keys] : 0;
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    if (key_offsets[k + 1] < key_offsets[k] || key_offsets[k + 1] > 0xffffffffull) {
+      set_error("bad key offsets");
+      return TFRG_E_ARG;
+    }
+    off[k] = (uint32_t)key_offsets[k];
+    hash[k] = fnv1a(key_blob + key_offsets[k], key_offsets[k + 1] - key_offsets[k]);
+    ks[4ull * k] = (int32_t)(key_flags ? (key_flags[k] & 1u) : 0u);
+    uint32_t j = hash[k] & (hsz - 1);
+    while (ht[j]) j = (j + 1) & (hsz - 1);
+    ht[j] = k + 1;
+  }
+  off[n_keys] = (uint32_t)blob_len;
+  for (uint32_t s = 0; s < n_slots; ++s) {
+    if (slot_key[s] >= n_keys || slot_kind[s] < 1 || slot_kind[s] > 3) {
+      set_error("bad slot");
+      return TFRG_E_ARG;
+    }
+    ks[4ull * slot_key[s] + slot_kind[s]] = (int32_t)s;
+  }
+  if (c->ht.ensure(hsz * 4) || c->key_hash.ensure(hash.size() * 4) || c->key_off.ensure(off.size() * 4) ||
+      c->key_blob.ensure(blob_len + 16) || c->key_slot.ensure(ks.size() * 4) || c->slot_kind.ensure(n_slots + 16)) {
+    set_error("schema allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(c->ht.p, ht.data(), hsz * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->key_hash.p, hash.data(), hash.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->key_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
+  if (blob_len) HIP_TRY(hipMemcpy(c->key_blob.p, key_blob, blob_len, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->key_slot.p, ks.data(), ks.size() * 4, hipMemcpyHostToDevice));
+  if (n_slots) HIP_TRY(hipMemcpy(c->slot_kind.p, slot_kind, n_slots, hipMemcpyHostToDevice));
+  c->n_keys = n_keys;
+  c->n_slots = n_slots;
+  c->ht_mask = hsz - 1;
+  return 0;
+}
+
+static DevSchema schema_view(const tfrg_ctx* c) {
+  DevSchema s;
+  s.n_keys = c->n_keys;
+  s.n_slots = c->n_slots;
+  s.ht_mask = c->ht_mask;
+  s.ht = c->ht.as<uint32_t>();
+  s.key_hash = c->key_hash.as<uint32_t>();
+  s.key_off = c->key_off.as<uint32_t>();
+  s.key_blob = c->key_blob.as<uint8_t>();
+  s.key_slot = c->key_slot.as<int32_t>();
+  s.slot_kind = c->slot_kind.as<uint8_t>();
+  return s;
+}
+
+int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_start,
+                       const uint64_t* d_end, uint32_t n, uint32_t flags, void* stream) {
+  if (!c) return TFRG_E_ARG;
+  if (nbytes >= (1ull << 32)) {
+    set_error("batch larger than 4 GiB: split it");
+    return TFRG_E_LIMIT;
+  }
+  if (c->n_keys == 0) {  // an empty table still needs valid (non-null) pointers
+    uint64_t z = 0;
+    int st = tfrg_set_schema(c, 0, nullptr, &z, nullptr, 0, nullptr, nullptr);
+    if (st) return st;
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
+  const uint32_t S = c->n_slots;
+  const uint64_t nn = n ? n : 1;
+  const uint32_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  const uint64_t cap_i64 = nbytes + 16, cap_f32 = nbytes / 4 + 16, cap_b = nbytes / 2 + 16;
+  // growing an arena buffer frees the old one: wait for work that may still read it
+  bool grow = c->status.cap < nn * 4 || c->aux.cap < nn * 8 || c->verdict.cap < nn ||
+              c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
+              c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
+              c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
+              c->granules.cap < (uint64_t)S * n_tiles * 8 + 8;
+  if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
+      c->count.ensure(S * nn * 4) || c->loc.ensure(S * nn * 8) || c->rs.ensure(S * (nn + 1) * 4) ||
+      c->slot_base.ensure((S + 1) * 8) || c->totals.ensure((S + 1) * 4) || c->kind_totals.ensure(32) ||
+      c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
+      c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->miss.ensure(kMissCap * 16ull) ||
+      c->info.ensure(kInfoCount * 4) || c->granules.ensure((uint64_t)S * n_tiles * 8 + 8) || c->ticket.ensure(16)) {
+    set_error("device allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
+  HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
+  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
+  HIP_TRY(hipMemsetAsync(c->ticket.p, 0, 16, st));
+  if (S && n_tiles) HIP_TRY(hipMemsetAsync(c->granules.p, 0, (size_t)S * n_tiles * 8, st));
+  if (S) HIP_TRY(hipMemsetAsync(c->totals.p, 0, S * 4, st));
+  if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
+
+  DevBatch b;
+  b.bytes = d_bytes;
+  b.nbytes = nbytes;
+  b.start = d_start;
+  b.end = d_end;
+  b.n = n;
+  b.flags = flags;
+  DevOut o;
+  o.status = c->status.as<int32_t>();
+  o.aux = c->aux.as<int64_t>();
+  o.verdict = c->verdict.as<uint8_t>();
+  o.order = c->order.as<uint16_t>();
+  o.count = c->count.as<uint32_t>();
+  o.loc = c->loc.as<uint2>();
+  o.rs = c->rs.as<uint32_t>();
+  o.slot_base = c->slot_base.as<uint64_t>();
+  o.totals = c->totals.as<uint32_t>();
+  o.kind_totals = c->kind_totals.as<uint64_t>();
+  o.i64 = c->i64.as<int64_t>();
+  o.f32 = c->f32.as<uint32_t>();
+  o.b_off = c->b_off.as<uint32_t>();
+  o.b_len = c->b_len.as<uint32_t>();
+  o.cap_i64 = cap_i64;
+  o.cap_f32 = cap_f32;
+  o.cap_b = cap_b;
+  o.big_list = c->big_list.as<uint32_t>();
+  o.miss = c->miss.as<uint32_t>();
+  o.miss_cap = kMissCap;
+  o.info = c->info.as<uint32_t>();
+  o.granules = c->granules.as<uint64_t>();
+  o.ticket = c->ticket.as<uint32_t>();
+  LaunchCfg cfg;
+  const uint64_t lane_blocks = (n + 255) / 256;
+  const uint64_t lane_cap = (uint64_t)c->num_cus * 8;
+  cfg.lane_grid = (int)(lane_blocks < 1 ? 1 : (lane_blocks < lane_cap ? lane_blocks : lane_cap));
+  const uint64_t wave_cap = (uint64_t)c->num_cus * 4;
+  const uint64_t wave_blocks = (n + 3) / 4;
+  cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
+  cfg.lane_max = c->lane_max;
+  if (n) {
+    hipError_t e = launch_decode(b, schema_view(c), o, cfg, c->crc_tab.as<uint32_t>(), c->consts.as<uint32_t>(), st);
+    if (e != hipSuccess) {
+      set_error(std::string("kernel launch: ") + hipGetErrorString(e));
+      return TFRG_E_HIP;
+    }
+  } else {
+    HIP_TRY(hipMemsetAsync(c->kind_totals.p, 0, 32, st));
+  }
+  c->n = n;
+  c->nbytes = nbytes;
+  c->cap_i64 = cap_i64;
+  c->cap_f32 = cap_f32;
+  c->cap_b = cap_b;
+  c->last_stream = st;
+  c->have_result = true;
+  return 0;
+}
+
+int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                     const uint64_t* h_end, uint32_t n, uint32_t flags, void* stream) {
+  if (!c) return TFRG_E_ARG;
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
+  const uint64_t pad = ((nbytes + 15) & ~15ull) + 16;
+  if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  if (c->in_bytes.ensure(pad) || c->in_start.ensure((uint64_t)(n ? n : 1) * 8) ||
+      c->in_end.ensure((uint64_t)(n ? n : 1) * 8)) {
+    set_error("staging allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  if (nbytes) HIP_TRY(hipMemcpyAsync(c->in_bytes.p, h_bytes, nbytes, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemsetAsync(c->in_bytes.as<uint8_t>() + nbytes, 0, pad - nbytes, st));
+  if (n) {
+    HIP_TRY(hipMemcpyAsync(c->in_start.p, h_start, (size_t)n * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c->in_end.p, h_end, (size_t)n * 8, hipMemcpyHostToDevice, st));
+  }
+  return tfrg_decode_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_start.as<uint64_t>(),
+                            c->in_end.as<uint64_t>(), n, flags, st);
+}
+
+int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
+  if (!c || !c->have_result) return TFRG_E_ARG;
+  HIP_TRY(hipSetDevice(c->device));
+  uint32_t h[kInfoCount] = {0};
+  uint64_t kt[4] = {0, 0, 0, 0};
+  HIP_TRY(hipMemcpyAsync(h, c->info.p, sizeof(h), hipMemcpyDeviceToHost, c->last_stream));
+  HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
+  HIP_TRY(hipStreamSynchronize(c->last_stream));
+  memset(info, 0, sizeof(*info));
+  info->n_records = c->n;
+  info->n_slots = c->n_slots;
+  info->n_errors = h[kInfoErrors];
+  info->first_error = h[kInfoFirstError];
+  info->n_miss_records = h[kInfoMissRecords];
+  info->n_miss_entries = h[kInfoMissEntries];
+  info->n_big = h[kInfoBig];
+  info->scan_timeout = h[kInfoScanTimeout];
+  for (int k = 0; k < 4; ++k) info->kind_totals[k] = kt[k];
+  info->nbytes = c->nbytes;
+  return 0;
+}
+
+int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
+  if (!c || !c->have_result) return TFRG_E_ARG;
+  d->status = c->status.as<int32_t>();
+  d->aux = c->aux.as<int64_t>();
+  d->verdict = c->verdict.as<uint8_t>();
+  d->order = c->order.as<uint16_t>();
+  d->row_splits = c->rs.as<uint32_t>();
+  d->slot_base = c->slot_base.as<uint64_t>();
+  d->i64 = c->i64.as<int64_t>();
+  d->f32 = c->f32.as<uint32_t>();
+  d->bytes_off = c->b_off.as<uint32_t>();
+  d->bytes_len = c->b_len.as<uint32_t>();
+  d->miss = c->miss.as<uint32_t>();
+  return 0;
+}
+
+int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
+  tfrg_info info;
+  int rc = tfrg_result_info(c, &info);
+  if (rc) return rc;
+  const hipStream_t st = c->last_stream;
+  const size_t n = c->n, S = c->n_slots;
+  auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+    if (!dst || !bytes) return hipSuccess;
+    return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
+  };
+  HIP_TRY(cp(h->status, c->status.p, n * 4));
+  HIP_TRY(cp(h->aux, c->aux.p, n * 8));
+  HIP_TRY(cp(h->verdict, c->verdict.p, n));
+  HIP_TRY(cp(h->order, c->order.p, S * n * 2));
+  HIP_TRY(cp(h->row_splits, c->rs.p, S * (n + 1) * 4));
+  HIP_TRY(cp(h->slot_base, c->slot_base.p, S * 8));
+  HIP_TRY(cp(h->i64, c->i64.p, info.kind_totals[TFRG_KIND_INT64] * 8));
+  HIP_TRY(cp(h->f32, c->f32.p, info.kind_totals[TFRG_KIND_FLOAT] * 4));
+  HIP_TRY(cp(h->bytes_off, c->b_off.p, info.kind_totals[TFRG_KIND_BYTES] * 4));
+  HIP_TRY(cp(h->bytes_len, c->b_len.p, info.kind_totals[TFRG_KIND_BYTES] * 4));
+  const size_t nm = info.n_miss_entries < kMissCap ? info.n_miss_entries : kMissCap;
+  HIP_TRY(cp(h->miss, c->miss.p, nm * 16));
+  HIP_TRY(hipStreamSynchronize(st));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,201 @@
+// tfrg_host.cpp — host-side native pieces of libtfrg: the TFRecord framing index over an mmap'd
+// file image (replaces cython/indexer.pyx:212-252, bit-exact), the .idx cache format
+// (indexer.pyx:255-328), CRC-32C and the TFRecord writer framing.
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <string>
+
+#include "../../include/tfrg.h"
+#include "crc32c.h"
+
+namespace tfrg {
+thread_local std::string g_last_error;
+void set_error(const std::string& s) { g_last_error = s; }
+
+// slice-by-8 host tables, built once
+struct HostCrc {
+  uint32_t t[8][256];
+  HostCrc() {
+    CrcTables T;
+    crc_make_tables(&T);
+    for (int v = 0; v < 256; ++v) t[0][v] = T.t[0][v];
+    for (int v = 0; v < 256; ++v) {
+      uint32_t c = t[0][v];
+      for (int j = 1; j < 8; ++j) {
+        c = (c >> 8) ^ t[0][c & 0xff];
+        t[j][v] = c;
+      }
+    }
+  }
+  uint32_t update(uint32_t c, const uint8_t* p, uint64_t n) const {
+    while (n && ((uintptr_t)p & 7)) {
+      c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+      --n;
+    }
+    while (n >= 8) {
+      uint64_t w;
+      memcpy(&w, p, 8);
+      w ^= c;
+      c = t[7][w & 0xff] ^ t[6][(w >> 8) & 0xff] ^ t[5][(w >> 16) & 0xff] ^ t[4][(w >> 24) & 0xff] ^
+          t[3][(w >> 32) & 0xff] ^ t[2][(w >> 40) & 0xff] ^ t[1][(w >> 48) & 0xff] ^ t[0][w >> 56];
+      p += 8;
+      n -= 8;
+    }
+    while (n--) c = t[0][(c ^ *p++) & 0xff] ^ (c >> 8);
+    return c;
+  }
+};
+static const HostCrc& host_crc() {
+  static const HostCrc h;
+  return h;
+}
+}  // namespace tfrg
+
+using namespace tfrg;
+
+extern "C" {
+
+int tfrg_abi_version(void) { return TFRG_ABI_VERSION; }
+const char* tfrg_last_error(void) { return g_last_error.c_str(); }
+void tfrg_free(void* p) { free(p); }
+
+uint32_t tfrg_crc32c(const uint8_t* p, uint64_t n) { return ~host_crc().update(0xffffffffu, p, n); }
+uint32_t tfrg_masked_crc32c(const uint8_t* p, uint64_t n) { return crc_mask(tfrg_crc32c(p, n)); }
+
+// The reference loop, with stdio semantics made explicit:
+//   start = ftell; fread(8) != 8 -> stop; fseek(+4) (past EOF is allowed);
+//   push (start, start + 16 + len, len); fseek(+(long)(len + 4)) fails -> stop.
+// A last record whose payload runs past EOF is therefore indexed (verified in the survey).
+int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out, int64_t cap) {
+  int64_t n = 0, pos = 0;
+  for (;;) {
+    if ((uint64_t)pos + 8 > size) break;
+    const uint64_t start = (uint64_t)pos;
+    uint64_t length;
+    memcpy(&length, file + pos, 8);
+    pos += 12;
+    if (n < cap) {
+      out[3 * n] = start;
+      out[3 * n + 1] = start + 16 + length;  // u64 arithmetic, as the reference
+      out[3 * n + 2] = length;
+    }
+    ++n;
+    const int64_t off = (int64_t)(length + 4);  // fseek's long offset
+    int64_t np;
+    if (__builtin_add_overflow(pos, off, &np) || np < 0) break;
+    pos = np;
+  }
+  return n;
+}
+
+int tfrg_index_file(const char* path, uint64_t** out_triples, int64_t* n) {
+  *out_triples = nullptr;
+  *n = 0;
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) {
+    set_error(std::string("Cannot open file: ") + path);
+    return TFRG_E_IO;
+  }
+  struct stat sb;
+  if (fstat(fd, &sb) != 0) {
+    close(fd);
+    set_error("fstat failed");
+    return TFRG_E_IO;
+  }
+  const uint64_t size = (uint64_t)sb.st_size;
+  const uint8_t* img = nullptr;
+  if (size) {
+    void* m = mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) {
+      close(fd);
+      set_error("mmap failed");
+      return TFRG_E_IO;
+    }
+    madvise(m, size, MADV_SEQUENTIAL);
+    img = (const uint8_t*)m;
+  }
+  close(fd);
+  // count first (cheap: touches 8 bytes per record), then fill
+  const int64_t cnt = tfrg_index_buffer(img, size, nullptr, 0);
+  uint64_t* out = (uint64_t*)malloc(sizeof(uint64_t) * 3 * (size_t)(cnt > 0 ? cnt : 1));
+  if (!out) {
+    if (img) munmap((void*)img, size);
+    set_error("out of memory");
+    return TFRG_E_NOMEM;
+  }
+  tfrg_index_buffer(img, size, out, cnt);
+  if (img) munmap((void*)img, size);
+  *out_triples = out;
+  *n = cnt;
+  return 0;
+}
+
+int tfrg_idx_save(const char* idx_path, const uint64_t* triples, int64_t n) {
+  FILE* f = fopen(idx_path, "wb");
+  if (!f) return TFRG_E_IO;
+  const size_t cnt = (size_t)n;
+  bool ok = fwrite(&cnt, sizeof(size_t), 1, f) == 1;
+  if (ok && cnt) ok = fwrite(triples, sizeof(uint64_t) * 3, cnt, f) == cnt;
+  fclose(f);
+  return ok ? 0 : TFRG_E_IO;
+}
+
+int tfrg_idx_load(const char* idx_path, uint64_t** out_triples, int64_t* n) {
+  *out_triples = nullptr;
+  *n = 0;
+  FILE* f = fopen(idx_path, "rb");
+  if (!f) {
+    set_error(std::string("Cannot open index file: ") + idx_path);
+    return TFRG_E_IO;
+  }
+  size_t cnt = 0;
+  if (fread(&cnt, sizeof(size_t), 1, f) != 1) {
+    fclose(f);
+    set_error("Failed to read index file header");
+    return TFRG_E_IO;
+  }
+  uint64_t* out = (uint64_t*)malloc(sizeof(uint64_t) * 3 * (cnt ? cnt : 1));
+  if (!out) {
+    fclose(f);
+    set_error("Failed to allocate memory for index");
+    return TFRG_E_NOMEM;
+  }
+  if (cnt && fread(out, sizeof(uint64_t) * 3, cnt, f) != cnt) {
+    free(out);
+    fclose(f);
+    set_error("Failed to read index pointers");
+    return TFRG_E_IO;
+  }
+  fclose(f);
+  *out_triples = out;
+  *n = (int64_t)cnt;
+  return 0;
+}
+
+int64_t tfrg_frame_records(const uint8_t* payloads, const uint64_t* offsets, int64_t n, int crc, uint8_t* out,
+                           int64_t out_cap) {
+  int64_t total = 0;
+  for (int64_t i = 0; i < n; ++i) total += 16 + (int64_t)(offsets[i + 1] - offsets[i]);
+  if (!out || total > out_cap) return total;
+  uint8_t* p = out;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t len = offsets[i + 1] - offsets[i];
+    memcpy(p, &len, 8);
+    const uint32_t lc = crc ? tfrg_masked_crc32c(p, 8) : 0u;
+    memcpy(p + 8, &lc, 4);
+    memcpy(p + 12, payloads + offsets[i], len);
+    const uint32_t dc = crc ? tfrg_masked_crc32c(payloads + offsets[i], len) : 0u;
+    memcpy(p + 12 + len, &dc, 4);
+    p += 16 + len;
+  }
+  return total;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// tfrg_internal.h — device-side views shared by the kernels (tfrg_kernels.hip) and the C-ABI
+// orchestration (tfrg_capi.cpp). Not part of the public ABI (include/tfrg.h is).
+#pragma once
+#include <stdint.h>
+#include <hip/hip_runtime.h>
+
+namespace tfrg {
+
+// Device key table (the "schema"): distinct key byte strings, each with up to one slot per kind.
+// A slot is one (key, kind) column of the columnar result.
+struct DevSchema {
+  uint32_t n_keys;
+  uint32_t n_slots;
+  uint32_t ht_mask;            // open-addressing table size - 1
+  const uint32_t* ht;          // [ht_mask+1] key_id + 1, 0 = empty
+  const uint32_t* key_hash;    // [n_keys] FNV-1a of the key bytes
+  const uint32_t* key_off;     // [n_keys+1] into key_blob
+  const uint8_t* key_blob;
+  const int32_t* key_slot;     // [n_keys*4]: [0] flags (bit0 invalid UTF-8), [1..3] slot per kind or -1
+  const uint8_t* slot_kind;    // [n_slots]
+};
+
+struct DevBatch {
+  const uint8_t* bytes;        // records (framed or bare payloads); readable to round_up(nbytes,16)
+  uint64_t nbytes;
+  const uint64_t* start;       // [n] absolute offsets into bytes
+  const uint64_t* end;         // [n]
+  uint32_t n;
+  uint32_t flags;
+};
+
+// Info counters (device, zeroed per decode)
+enum InfoIdx : uint32_t {
+  kInfoErrors = 0,       // records with a decode error (reference exception / UB status)
+  kInfoFirstError = 1,   // lowest record index with an error (atomicMin, init 0xffffffff)
+  kInfoMissRecords = 2,  // records with a schema miss
+  kInfoMissEntries = 3,  // miss entries appended (may exceed capacity)
+  kInfoBig = 4,          // records routed to the wave-per-record kernels
+  kInfoScanTimeout = 5,  // look-back spin gave up (must stay 0)
+  kInfoCount = 16
+};
+
+struct DevOut {
+  int32_t* status;       // [n]
+  int64_t* aux;          // [n] error detail
+  uint8_t* verdict;      // [n] tfrg_verdict bits
+  uint16_t* order;       // [n_slots][n]  0 = absent, else 1 + rank in the record's key order
+  uint32_t* count;       // [n_slots][n]
+  uint2* loc;            // [n_slots][n]  (payload-relative offset, length) of the list message
+  uint32_t* rs;          // [n_slots][n+1] row splits (exclusive prefix of count)
+  uint64_t* slot_base;   // [n_slots] element base of each slot inside its kind's value array
+  uint32_t* totals;      // [n_slots]
+  uint64_t* kind_totals; // [4]
+  int64_t* i64;          // int64 values
+  uint32_t* f32;         // float values (raw bits)
+  uint32_t* b_off;       // bytes_list element views: absolute offset into bytes
+  uint32_t* b_len;
+  uint64_t cap_i64, cap_f32, cap_b;
+  uint32_t* big_list;    // records for the wave-per-record kernels
+  uint32_t* miss;        // [miss_cap][4] (record, kind, key abs offset, key length)
+  uint32_t miss_cap;
+  uint32_t* info;        // [kInfoCount]
+  uint64_t* granules;    // [n_slots][n_tiles] scan look-back state
+  uint32_t* ticket;      // scan tile ticket
+};
+
+// flags (mirrors include/tfrg.h)
+constexpr uint32_t kFlagPayloadOnly = 1u;
+constexpr uint32_t kFlagSpecVarint = 2u;
+constexpr uint32_t kFlagNoCrc = 4u;
+
+constexpr int kScanBlock = 256;
+constexpr int kScanItems = 8;
+constexpr uint32_t kScanTile = kScanBlock * kScanItems;
+
+// launchers (tfrg_kernels.hip)
+struct LaunchCfg {
+  int lane_grid;
+  int wave_grid;
+  uint32_t lane_max;       // records above this size go to the wave kernels
+};
+
+hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
+                         const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream);
+
+}  // namespace tfrg

@@ -1,0 +1,854 @@
+// tfrg_kernels.hip — gfx950 kernels for the TFRecord -> tf.train.Example -> Feature path.
+//
+// Pipeline for one batch of framed records resident in HBM (launch_decode):
+//   1. k_lane_count  : one LANE per record (records <= lane_max bytes). Framing check, masked
+//                      CRC-32C of length and payload (slice-by-4, bank-replicated LDS tables),
+//                      then a reference-exact walk of Example -> Features -> map entries ->
+//                      Feature -> value list (decoder.pyx:53-300) that validates every level in
+//                      the reference's error precedence and records, per (key, kind) slot, the
+//                      value count, the list location and the key's dict position.
+//                      Larger records are appended to a work list.
+//   2. k_wave_count  : one WAVEFRONT per large record: the CRC is split over 64 lanes in 16-byte
+//                      chunks (coalesced 1 KiB rounds) and recombined with GF(2) shift operators;
+//                      the structure walk runs wave-uniform.
+//   3. k_scan        : per-slot exclusive scan of the counts (single pass, decoupled look-back
+//                      over 8-byte {status,value} granules, agent-scope relaxed atomics).
+//   4. k_base        : per-kind column bases.
+//   5. k_lane_gather / k_wave_gather : write the int64 / float / bytes-view values of every
+//                      present slot into per-slot contiguous columns.
+//
+// All walks share one templated walker so the lane and wave paths cannot drift apart.
+#include <hip/hip_runtime.h>
+#include "tfrg_internal.h"
+#include "crc32c.h"
+#include "../../include/tfrg_status.h"
+
+namespace tfrg {
+
+// ------------------------------------------------------------------------------------------------
+// Byte source: payload bytes of one record with the reference's out-of-range behaviour
+// (index == L reads the CPython NUL terminator, index > L is reference UB), read through a
+// per-lane 16-byte aligned window so that sequential parsing issues one 16 B load per 16 bytes.
+// ------------------------------------------------------------------------------------------------
+struct Src {
+  const uint8_t* buf;
+  uint64_t p0;  // absolute payload start
+  int64_t L;    // payload length
+  uint64_t wb;  // window base (absolute, 16-aligned)
+  uint4 w;
+  bool ub;
+
+  __device__ __forceinline__ void init(const uint8_t* b, uint64_t p, int64_t len) {
+    buf = b;
+    p0 = p;
+    L = len;
+    wb = ~0ull;
+    ub = false;
+  }
+  __device__ __forceinline__ uint32_t raw(uint64_t a) {
+    const uint64_t base = a & ~15ull;
+    if (base != wb) {
+      w = *reinterpret_cast<const uint4*>(buf + base);
+      wb = base;
+    }
+    const uint32_t k = (uint32_t)(a >> 2) & 3u;
+    const uint32_t d = k == 0 ? w.x : (k == 1 ? w.y : (k == 2 ? w.z : w.w));
+    return (d >> ((a & 3u) * 8u)) & 0xffu;
+  }
+  __device__ __forceinline__ uint32_t at(int64_t i) {
+    if (i >= L) {
+      ub |= (i > L);
+      return 0u;
+    }
+    return raw(p0 + (uint64_t)i);
+  }
+  // 4 payload bytes at i (caller guarantees i + 4 <= L)
+  __device__ __forceinline__ uint32_t u32(int64_t i) {
+    return at(i) | (at(i + 1) << 8) | (at(i + 2) << 16) | (at(i + 3) << 24);
+  }
+};
+
+// decode_varint (decoder.pyx:34-50). COMPAT reproduces the reference's int-width shift:
+// term = (int32)((b & 0x7F) << (shift & 31)), sign-extended.
+template <bool COMPAT>
+__device__ __forceinline__ int rd_varint(Src& s, int64_t& pos, int64_t& val) {
+  int64_t r = 0;
+  int shift = 0;
+  for (;;) {
+    const uint32_t b = s.at(pos);
+    ++pos;
+    const uint32_t g = b & 0x7fu;
+    if (COMPAT) {
+      r |= (int64_t)(int32_t)(g << (shift & 31));
+    } else if (shift < 64) {
+      r |= (int64_t)((uint64_t)g << shift);
+    }
+    if (!(b & 0x80u)) break;
+    shift += 7;
+    if (shift >= 64) return TFRG_ERR_VARINT_TOO_MANY;
+  }
+  if (s.ub) return TFRG_UB_READ_PAST_END;
+  val = r;
+  return TFRG_OK;
+}
+
+// same control flow without assembling the value (counting passes)
+__device__ __forceinline__ int skip_varint(Src& s, int64_t& pos) {
+  int shift = 0;
+  for (;;) {
+    const uint32_t b = s.at(pos);
+    ++pos;
+    if (!(b & 0x80u)) break;
+    shift += 7;
+    if (shift >= 64) return TFRG_ERR_VARINT_TOO_MANY;
+  }
+  return s.ub ? TFRG_UB_READ_PAST_END : TFRG_OK;
+}
+
+struct Fld {
+  int64_t fn, wt, off, len;
+};
+
+// One iteration of decode_message (decoder.pyx:69-104).
+template <bool COMPAT>
+__device__ __forceinline__ int rd_field(Src& s, int64_t& pos, int64_t end, Fld& f, int64_t& aux) {
+  int64_t key;
+  int st = rd_varint<COMPAT>(s, pos, key);
+  if (st) return st;
+  f.fn = key >> 3;
+  f.wt = key & 7;
+  if (f.wt == 1) {
+    if (pos + 8 > end) return TFRG_ERR_EOB_FIXED64;
+    f.off = pos;
+    f.len = 8;
+    pos += 8;
+    return TFRG_OK;
+  }
+  if (f.wt == 2) {
+    int64_t len;
+    st = rd_varint<COMPAT>(s, pos, len);
+    if (st) return st;
+    if (COMPAT) {
+      if (pos + len > end) return TFRG_ERR_EOB_LEN;  // |len| < 2^31 here: no overflow
+      if (len < 0) return TFRG_UB_NEGATIVE_LENGTH;   // passes the check, then pos moves back
+    } else {
+      if (pos > end || (uint64_t)len > (uint64_t)(end - pos)) return TFRG_ERR_EOB_LEN;
+    }
+    f.off = pos;
+    f.len = len;
+    pos += len;
+    return TFRG_OK;
+  }
+  if (f.wt == 5) {
+    if (pos + 4 > end) return TFRG_ERR_EOB_FIXED32;
+    f.off = pos;
+    f.len = 4;
+    pos += 4;
+    return TFRG_OK;
+  }
+  aux = f.wt;
+  return TFRG_ERR_WIRE_TYPE;
+}
+
+// decode_message validation pass: every tag/length of one level before any child is parsed,
+// which is the reference's level-by-level error precedence.
+template <bool COMPAT>
+__device__ int scan_msg(Src& s, int64_t pos, int64_t end, int64_t& aux) {
+  Fld f;
+  while (pos < end) {
+    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
+    if (st) return st;
+  }
+  return TFRG_OK;
+}
+
+// bytes/float/int64 list (decoder.pyx:203-300): validation + element count.
+template <bool COMPAT>
+__device__ int list_count(Src& s, int kind, int64_t o, int64_t n, int64_t& aux, uint32_t& count) {
+  const int64_t end = o + n;
+  int st = scan_msg<COMPAT>(s, o, end, aux);
+  if (st) return st;
+  uint64_t c = 0;
+  int64_t pos = o;
+  Fld f;
+  while (pos < end) {
+    rd_field<COMPAT>(s, pos, end, f, aux);  // validated above
+    if (f.fn != 1) continue;
+    if (kind == TFRG_KIND_BYTES) {
+      if (f.wt != 2) return TFRG_ERR_WT_BYTES_LIST;
+      ++c;
+    } else if (kind == TFRG_KIND_FLOAT) {
+      if (f.wt == 2) c += (uint64_t)(f.len >> 2);  // floor(len/4): trailing bytes dropped
+      else if (f.wt == 5) ++c;
+      else return TFRG_ERR_WT_FLOAT_LIST;
+    } else {
+      if (f.wt != 2) return TFRG_ERR_WT_INT64_LIST;
+      // packed varints until p >= chunk end; the last one may run past the chunk (no bound)
+      int64_t p = f.off;
+      const int64_t e = f.off + f.len;
+      while (p < e) {
+        st = skip_varint(s, p);
+        if (st) return st;
+        ++c;
+      }
+    }
+  }
+  count = (uint32_t)c;
+  return TFRG_OK;
+}
+
+// feature_from_bytes (decoder.pyx:169-199): kind = field number of the FIRST field.
+template <bool COMPAT>
+__device__ int walk_feature(Src& s, int64_t o, int64_t n, int64_t& aux, int& kind, int64_t& lo,
+                            int64_t& ll, uint32_t& count) {
+  const int64_t end = o + n;
+  int64_t pos = o;
+  Fld f, g0;
+  int cnt = 0;
+  while (pos < end) {
+    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
+    if (st) return st;
+    if (cnt == 0) g0 = f;
+    ++cnt;
+  }
+  if (cnt == 0) return TFRG_UB_EMPTY_FEATURE;
+  if (g0.fn < 1 || g0.fn > 3) return TFRG_ERR_FEATURE_FIELD;
+  kind = (int)g0.fn;
+  lo = g0.off;
+  ll = g0.len;
+  return list_count<COMPAT>(s, kind, g0.off, g0.len, aux, count);
+}
+
+// parse_map_entry (decoder.pyx:153-166): positional fields[0] = key, fields[1] = value.
+template <bool COMPAT, class Sink>
+__device__ int walk_entry(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
+  const int64_t end = o + n;
+  int64_t pos = o;
+  Fld f, f0, f1;
+  int cnt = 0;
+  while (pos < end) {
+    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
+    if (st) return st;
+    if (cnt == 0) f0 = f;
+    else if (cnt == 1) f1 = f;
+    ++cnt;
+  }
+  if (cnt < 2) return TFRG_UB_SHORT_MAP_ENTRY;
+  const int kid = sink.lookup(s, f0.off, f0.len);
+  if (kid == -2) {  // interned as invalid UTF-8: bytes(key).decode('utf-8') raises here
+    aux = (int64_t)(((uint64_t)f0.off << 32) | (uint64_t)(uint32_t)f0.len);
+    return TFRG_ERR_KEY_UTF8;
+  }
+  int kind = 0;
+  int64_t lo = 0, ll = 0;
+  uint32_t count = 0;
+  const int st = walk_feature<COMPAT>(s, f1.off, f1.len, aux, kind, lo, ll, count);
+  if (st) return st;
+  return sink.insert(kid, kind, lo, ll, count, f0.off, f0.len);
+}
+
+// features_from_bytes (decoder.pyx:130-150)
+template <bool COMPAT, class Sink>
+__device__ int walk_features(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
+  const int64_t end = o + n;
+  int st = scan_msg<COMPAT>(s, o, end, aux);
+  if (st) return st;
+  sink.reset();  // a repeated Features field replaces the dict, never merges (decoder.pyx:121)
+  int64_t pos = o;
+  Fld f;
+  while (pos < end) {
+    rd_field<COMPAT>(s, pos, end, f, aux);
+    if (f.fn != 1) continue;
+    if (f.wt != 2) return TFRG_ERR_WT_FEATURE;
+    st = walk_entry<COMPAT>(s, sink, f.off, f.len, aux);
+    if (st) return st;
+  }
+  return TFRG_OK;
+}
+
+// example_from_bytes (decoder.pyx:107-127) + Feature(proto.features.feature) (feature.py:106)
+template <bool COMPAT, class Sink>
+__device__ int walk_example(Src& s, Sink& sink, int64_t& aux) {
+  const int64_t L = s.L;
+  int st = scan_msg<COMPAT>(s, 0, L, aux);
+  if (st) return st;
+  bool have = false;
+  int64_t pos = 0;
+  Fld f;
+  while (pos < L) {
+    rd_field<COMPAT>(s, pos, L, f, aux);
+    if (f.fn != 1) continue;
+    if (f.wt != 2) return TFRG_ERR_WT_FEATURES;
+    st = walk_features<COMPAT>(s, sink, f.off, f.len, aux);
+    if (st) return st;
+    have = true;
+  }
+  return have ? TFRG_OK : TFRG_ERR_FEATURES_NONE;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Count sink: dict semantics (insertion order, last value wins, first position kept) over
+// (key, kind) slots, with the per-record rank state in LDS.
+// ------------------------------------------------------------------------------------------------
+struct CountSink {
+  const DevSchema* sc;
+  const DevOut* o;
+  uint16_t* ord;     // LDS, ord[slot * ostride]
+  uint32_t ostride;
+  uint32_t rank;
+  uint32_t n, r;
+  uint64_t p0;
+  bool miss;
+  bool leader;       // issues global writes and atomics
+
+  __device__ __forceinline__ void reset() {
+    for (uint32_t k = 0; k < sc->n_slots; ++k) ord[k * ostride] = 0;
+    rank = 0;
+  }
+
+  // key bytes -> key id; -1 unknown, -2 interned as invalid UTF-8
+  __device__ int lookup(Src& s, int64_t off, int64_t len) {
+    uint32_t h = 2166136261u;
+    for (int64_t i = 0; i < len; ++i) h = (h ^ s.at(off + i)) * 16777619u;
+    if (sc->n_keys == 0) return -1;
+    uint32_t j = h & sc->ht_mask;
+    for (uint32_t probe = 0; probe <= sc->ht_mask; ++probe) {
+      const uint32_t e = sc->ht[j];
+      if (!e) return -1;
+      const uint32_t kid = e - 1;
+      const uint32_t ko = sc->key_off[kid];
+      if (sc->key_hash[kid] == h && (int64_t)(sc->key_off[kid + 1] - ko) == len) {
+        const uint8_t* kb = sc->key_blob + ko;
+        bool eq = true;
+        for (int64_t i = 0; i < len && eq; ++i) eq = s.at(off + i) == kb[i];
+        if (eq) return (sc->key_slot[kid * 4] & 1) ? -2 : (int)kid;
+      }
+      j = (j + 1) & sc->ht_mask;
+    }
+    return -1;
+  }
+
+  __device__ int insert(int kid, int kind, int64_t lo, int64_t ll, uint32_t count, int64_t koff,
+                        int64_t klen) {
+    const int slot = kid >= 0 ? sc->key_slot[kid * 4 + kind] : -1;
+    if (slot < 0) {  // schema miss: report the (key, kind) so the host can intern it
+      miss = true;
+      if (leader) {
+        const uint32_t i = atomicAdd(&o->info[kInfoMissEntries], 1u);
+        if (i < o->miss_cap) {
+          uint32_t* m = o->miss + 4ull * i;
+          m[0] = r;
+          m[1] = (uint32_t)kind;
+          m[2] = (uint32_t)(p0 + (uint64_t)koff);
+          m[3] = (uint32_t)klen;
+        }
+      }
+      return TFRG_OK;
+    }
+    uint32_t rk = 0;
+    for (int k = 1; k <= 3; ++k) {  // duplicate key (any kind): keep its first position
+      const int s2 = sc->key_slot[kid * 4 + k];
+      if (s2 >= 0) {
+        const uint32_t v = ord[(uint32_t)s2 * ostride];
+        if (v) {
+          rk = v;
+          ord[(uint32_t)s2 * ostride] = 0;
+        }
+      }
+    }
+    if (!rk) {
+      if (rank >= 65534u) return TFRG_ST_LIMIT;
+      rk = ++rank;
+    }
+    ord[(uint32_t)slot * ostride] = (uint16_t)rk;
+    if (leader) {
+      const size_t at = (size_t)slot * n + r;
+      o->count[at] = count;
+      o->loc[at] = make_uint2((uint32_t)lo, (uint32_t)ll);
+    }
+    return TFRG_OK;
+  }
+
+  __device__ void finalize(bool ok) {
+    for (uint32_t k = 0; k < sc->n_slots; ++k) {
+      const uint32_t v = ok ? ord[k * ostride] : 0u;
+      if (leader) {
+        const size_t at = (size_t)k * n + r;
+        o->order[at] = (uint16_t)v;
+        if (!v) o->count[at] = 0;
+      }
+    }
+  }
+};
+
+// ------------------------------------------------------------------------------------------------
+// CRC-32C helpers
+// ------------------------------------------------------------------------------------------------
+// LDS table view with R-fold bank replication: entry (j, v) copy c at dword ((j*256+v)*R + c).
+// Lane l reads copy l % R, so up to R lanes of a 32-lane group never collide on a bank.
+template <int R>
+struct LdsTab {
+  const uint32_t* t;
+  uint32_t c;
+  __device__ __forceinline__ uint32_t operator()(uint32_t j, uint32_t v) const { return t[((j << 8) + v) * R + c]; }
+  __device__ __forceinline__ uint32_t step4(uint32_t x) const {
+    return (*this)(3, x & 0xffu) ^ (*this)(2, (x >> 8) & 0xffu) ^ (*this)(1, (x >> 16) & 0xffu) ^ (*this)(0, x >> 24);
+  }
+  __device__ __forceinline__ uint32_t step1(uint32_t c_, uint32_t byte) const {
+    return (*this)(0, (c_ ^ byte) & 0xffu) ^ (c_ >> 8);
+  }
+};
+
+// Serial CRC-32C of absolute bytes [a, b) by one lane: aligned 16 B loads, slice-by-4 for whole
+// words, byte steps at the unaligned edges.
+template <int R>
+__device__ uint32_t crc_serial(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<R>& T) {
+  uint32_t c = 0xffffffffu;
+  for (uint64_t q = a & ~15ull; q < b; q += 16) {
+    const uint4 w = *reinterpret_cast<const uint4*>(buf + q);
+    const uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t wa = q + 4ull * k;
+      if (wa >= a && wa + 4 <= b) {
+        c = T.step4(c ^ ws[k]);
+      } else if (wa + 4 > a && wa < b) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t ba = wa + j;
+          if (ba >= a && ba < b) c = T.step1(c, ws[k] >> (8 * j));
+        }
+      }
+    }
+  }
+  return ~c;
+}
+
+__device__ __forceinline__ uint32_t load_u32_unaligned(const uint8_t* buf, uint64_t a) {
+  uint32_t v = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v |= (uint32_t)buf[a + j] << (8 * j);
+  return v;
+}
+__device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* buf, uint64_t a) {
+  return (uint64_t)load_u32_unaligned(buf, a) | ((uint64_t)load_u32_unaligned(buf, a + 4) << 32);
+}
+
+// Wavefront CRC-32C of absolute bytes [a, b), b - a >= 64. Chunks are the buffer's aligned
+// 16-byte blocks; rounds of 64 chunks are taken from the END so that lane l's chunk in the last
+// round is followed by exactly l chunks. Each lane keeps S_l <- S_l (x) x^8192 ^ U(0, chunk); the
+// payload is then  xor_l S_l (x) x^(128 l), un-shifted by the z zero bytes padding the last chunk.
+// Leading bytes before a are zero (free for a zero initial state); the first 4 payload bytes are
+// inverted (the ~0 initial state).
+__device__ uint32_t crc_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
+                             const uint32_t* A /* LDS [4][256]: (x) x^8192 */, const uint32_t* consts,
+                             uint32_t lane) {
+  const uint64_t c0 = a >> 4, c1 = (b - 1) >> 4;
+  const uint64_t nch = c1 - c0 + 1;
+  const int64_t rounds = (int64_t)((nch + 63) >> 6);
+  uint32_t S = 0;
+  for (int64_t k = rounds - 1; k >= 0; --k) {
+    const int64_t ch = (int64_t)c1 - 64 * k - (int64_t)lane;
+    uint32_t Rc = 0;
+    if (ch >= (int64_t)c0) {
+      const uint64_t q = (uint64_t)ch << 4;
+      const uint4 w = *reinterpret_cast<const uint4*>(buf + q);
+      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      if (q < a + 4 || q + 16 > b) {  // edge chunk: mask outside bytes, invert the first 4
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+          uint32_t keep = 0, inv = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint64_t ba = q + 4ull * k2 + j;
+            if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
+            if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
+          }
+          ws[k2] = (ws[k2] & keep) ^ inv;
+        }
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
+    }
+    S = A[S & 0xffu] ^ A[256 + ((S >> 8) & 0xffu)] ^ A[512 + ((S >> 16) & 0xffu)] ^ A[768 + (S >> 24)] ^ Rc;
+  }
+  uint32_t t = gf_mul(S, consts[lane]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
+  const uint32_t z = (uint32_t)(16 * (c1 + 1) - b);
+  t = gf_mul(t, consts[64 + z]);
+  return ~t;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-record framing: payload range, verdict bits, read errors.
+// ------------------------------------------------------------------------------------------------
+struct RecView {
+  uint64_t st, e;   // absolute [st, e) clamped to the buffer
+  uint64_t p0;
+  int64_t L;
+  int status;
+  uint32_t verdict;
+};
+
+__device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
+  RecView v;
+  const uint64_t st = B.start[r], en = B.end[r];
+  v.st = st;
+  v.status = TFRG_OK;
+  v.verdict = 0;
+  const bool framed = !(B.flags & kFlagPayloadOnly);
+  if (st > en || (framed ? st >= B.nbytes : en > B.nbytes)) {  // reader.py:48-49 empty read
+    v.status = TFRG_ERR_READ;
+    v.e = st;
+    v.p0 = st;
+    v.L = 0;
+    return v;
+  }
+  v.e = en < B.nbytes ? en : B.nbytes;
+  if (en > B.nbytes) v.verdict |= TFRG_V_TRUNCATED;
+  if (framed) {  // reader.py:55: data = example_data[12:-4]
+    const uint64_t D = v.e - st;
+    v.p0 = st + 12;
+    v.L = D >= 16 ? (int64_t)(D - 16) : 0;
+  } else {
+    v.p0 = st;
+    v.L = (int64_t)(v.e - st);
+  }
+  return v;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Kernels
+// ------------------------------------------------------------------------------------------------
+constexpr int kLaneBlock = 256;
+constexpr int kWaveBlock = 256;
+constexpr int kWavesPerBlock = kWaveBlock / 64;
+
+__device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int status, int64_t aux,
+                                              uint32_t verdict) {
+  o.status[r] = status;
+  o.aux[r] = aux;
+  o.verdict[r] = (uint8_t)verdict;
+  if (status == TFRG_ST_SCHEMA_MISS) {
+    atomicAdd(&o.info[kInfoMissRecords], 1u);
+  } else if (status != TFRG_OK) {
+    atomicAdd(&o.info[kInfoErrors], 1u);
+    atomicMin(&o.info[kInfoFirstError], r);
+  }
+}
+
+template <int R, bool COMPAT>
+__global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+                                                           const uint32_t* __restrict__ crc_tab,
+                                                           uint32_t lane_max) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* tab = lds;                                           // 1024 * R dwords
+  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 1024 * R);   // [n_slots][kLaneBlock]
+  for (uint32_t i = threadIdx.x; i < 1024u * R; i += kLaneBlock) tab[i] = crc_tab[i / R];
+  __syncthreads();
+  const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
+  const bool framed = !(B.flags & kFlagPayloadOnly);
+  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
+
+  for (uint64_t ri = (uint64_t)blockIdx.x * kLaneBlock + threadIdx.x; ri < B.n;
+       ri += (uint64_t)gridDim.x * kLaneBlock) {
+    const uint32_t r = (uint32_t)ri;
+    RecView v = rec_view(B, r);
+    if (v.status == TFRG_OK && v.e - v.st > lane_max) {  // large record: wave kernel
+      const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
+      o.big_list[i] = r;
+      continue;
+    }
+    int64_t aux = 0;
+    CountSink sink{&sc, &o, ord + threadIdx.x, kLaneBlock, 0, B.n, r, v.p0, false, true};
+    int status = v.status;
+    if (status == TFRG_OK) {
+      if (framed) {
+        const uint64_t D = v.e - v.st;
+        if (D >= 8) {
+          const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
+          if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+          if (do_crc && D >= 12) {
+            const uint32_t c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
+            if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
+          }
+          if (do_crc && D >= 16) {
+            const uint32_t c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
+            if (crc_mask(c) == load_u32_unaligned(B.bytes, v.e - 4)) v.verdict |= TFRG_V_DATA_CRC;
+          }
+        }
+      }
+      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[k * kLaneBlock] = 0;
+      Src s;
+      s.init(B.bytes, v.p0, v.L);
+      status = walk_example<COMPAT>(s, sink, aux);
+      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+    }
+    sink.finalize(status == TFRG_OK);
+    record_result(o, r, status, aux, v.verdict);
+  }
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
+                                                          const uint32_t* __restrict__ crc_tab,
+                                                          const uint32_t* __restrict__ consts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* tab = lds;          // [4][256] slice-by-4
+  uint32_t* A = lds + 1024;     // [4][256] (x) x^8192
+  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 2048);  // [waves][n_slots]
+  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
+  __syncthreads();
+  const LdsTab<1> T{tab, 0};
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  const uint32_t nbig = o.info[kInfoBig];
+  const bool framed = !(B.flags & kFlagPayloadOnly);
+  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
+  uint16_t* word = ord + wib * sc.n_slots;
+
+  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
+    const uint32_t r = o.big_list[i];
+    RecView v = rec_view(B, r);
+    int64_t aux = 0;
+    CountSink sink{&sc, &o, word, 1, 0, B.n, r, v.p0, false, lane == 0};
+    if (framed) {
+      const uint64_t D = v.e - v.st;
+      if (D >= 8) {
+        const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
+        if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+        if (do_crc && D >= 12) {
+          const uint32_t c = crc_serial<1>(B.bytes, v.st, v.st + 8, T);
+          if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
+        }
+        if (do_crc && D >= 16) {
+          const uint64_t a = v.p0, b = v.e - 4;
+          const uint32_t c = (b - a >= 64) ? crc_wave(B.bytes, a, b, T, A, consts, lane)
+                                           : crc_serial<1>(B.bytes, a, b, T);
+          if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
+        }
+      }
+    }
+    for (uint32_t k = lane; k < sc.n_slots; k += 64) word[k] = 0;
+    __builtin_amdgcn_wave_barrier();
+    Src s;
+    s.init(B.bytes, v.p0, v.L);
+    int status = walk_example<COMPAT>(s, sink, aux);
+    if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+    __builtin_amdgcn_wave_barrier();
+    sink.finalize(status == TFRG_OK);
+    if (lane == 0) record_result(o, r, status, aux, v.verdict);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Per-slot exclusive scan, single pass with decoupled look-back.
+// Granule = {status:32 | value:32}; status 1 = tile aggregate, 2 = inclusive prefix. Written and
+// read with relaxed agent-scope 8-byte atomics: the data is the flag (Guideline 16 R2). Tiles are
+// taken in ticket order, so every tile a block waits on is already resident.
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict__ count, uint32_t* rs,
+                                                     uint32_t* totals, uint64_t* gran, uint32_t* ticket,
+                                                     uint32_t* info, uint32_t n, uint32_t n_tiles) {
+  __shared__ uint32_t s_t, s_prefix;
+  __shared__ uint32_t s_wsum[kScanBlock / 64];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
+  if (tid == 0) s_t = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t t = s_t;
+  const uint32_t slot = t / n_tiles, tile = t % n_tiles;
+  const uint32_t* c = count + (size_t)slot * n;
+  uint32_t* out = rs + (size_t)slot * (n + 1);
+  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
+  uint32_t v[kScanItems];
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const uint64_t idx = base + i;
+    v[i] = idx < n ? c[idx] : 0u;
+    sum += v[i];
+  }
+  // block exclusive scan of the per-thread sums
+  uint32_t incl = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wsum[wid] = incl;
+  __syncthreads();
+  uint32_t wpre = 0, agg = 0;
+#pragma unroll
+  for (int w = 0; w < kScanBlock / 64; ++w) {
+    if ((uint32_t)w < wid) wpre += s_wsum[w];
+    agg += s_wsum[w];
+  }
+  const uint32_t excl = wpre + incl - sum;
+  if (tid == 0) {
+    uint64_t* g = gran + (size_t)slot * n_tiles;
+    uint32_t prefix = 0;
+    if (tile == 0) {
+      __hip_atomic_store(&g[0], (2ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&g[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      int64_t j = (int64_t)tile - 1;
+      uint32_t spins = 0;
+      while (j >= 0) {
+        const uint64_t x = __hip_atomic_load(&g[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t stt = (uint32_t)(x >> 32);
+        if (stt == 0) {
+          if (++spins > (1u << 22)) {  // never hang the GPU: give up and flag
+            atomicAdd(&info[kInfoScanTimeout], 1u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+          continue;
+        }
+        prefix += (uint32_t)x;
+        if (stt == 2) break;
+        --j;
+      }
+      __hip_atomic_store(&g[tile], (2ull << 32) | (uint64_t)(prefix + agg), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_prefix = prefix;
+  }
+  __syncthreads();
+  uint32_t run = s_prefix + excl;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) {
+    const uint64_t idx = base + i;
+    if (idx < n) out[idx] = run;
+    run += v[i];
+  }
+  if (tile == n_tiles - 1 && tid == kScanBlock - 1) {
+    out[n] = run;
+    totals[slot] = run;
+  }
+}
+
+__global__ void k_base(const uint32_t* totals, const uint8_t* slot_kind, uint64_t* slot_base,
+                       uint64_t* kind_totals, uint32_t n_slots) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  uint64_t acc[4] = {0, 0, 0, 0};
+  for (uint32_t s = 0; s < n_slots; ++s) {
+    const uint32_t k = slot_kind[s] & 3u;
+    slot_base[s] = acc[k];
+    acc[k] += totals[s];
+  }
+  for (int k = 0; k < 4; ++k) kind_totals[k] = acc[k];
+}
+
+// ------------------------------------------------------------------------------------------------
+// Gather: decode the (validated) list message of every present slot into its column.
+// ------------------------------------------------------------------------------------------------
+template <bool COMPAT>
+__device__ void list_gather(Src& s, const DevOut& o, int kind, int64_t lo, int64_t ll, uint64_t dst) {
+  const int64_t end = lo + ll;
+  int64_t pos = lo, aux = 0;
+  Fld f;
+  while (pos < end) {
+    rd_field<COMPAT>(s, pos, end, f, aux);
+    if (f.fn != 1) continue;
+    if (kind == TFRG_KIND_BYTES) {
+      if (dst < o.cap_b) {
+        o.b_off[dst] = (uint32_t)(s.p0 + (uint64_t)f.off);
+        o.b_len[dst] = (uint32_t)f.len;
+      }
+      ++dst;
+    } else if (kind == TFRG_KIND_FLOAT) {
+      const int64_t m = f.wt == 2 ? (f.len >> 2) : 1;
+      for (int64_t i = 0; i < m; ++i) {
+        if (dst < o.cap_f32) o.f32[dst] = s.u32(f.off + 4 * i);
+        ++dst;
+      }
+    } else {
+      int64_t p = f.off;
+      const int64_t e = f.off + f.len;
+      while (p < e) {
+        int64_t val = 0;
+        rd_varint<COMPAT>(s, p, val);
+        if (dst < o.cap_i64) o.i64[dst] = val;
+        ++dst;
+      }
+    }
+  }
+}
+
+template <bool COMPAT>
+__device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o,
+                                              uint32_t r, const RecView& v) {
+  Src s;
+  s.init(B.bytes, v.p0, v.L);
+  for (uint32_t k = 0; k < sc.n_slots; ++k) {
+    const size_t at = (size_t)k * B.n + r;
+    if (!o.order[at]) continue;
+    const uint2 lc = o.loc[at];
+    const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+    list_gather<COMPAT>(s, o, sc.slot_kind[k], (int64_t)lc.x, (int64_t)lc.y, dst);
+  }
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchema sc, DevOut o,
+                                                            uint32_t lane_max) {
+  for (uint64_t ri = (uint64_t)blockIdx.x * kLaneBlock + threadIdx.x; ri < B.n;
+       ri += (uint64_t)gridDim.x * kLaneBlock) {
+    const uint32_t r = (uint32_t)ri;
+    const RecView v = rec_view(B, r);
+    if (v.status != TFRG_OK || v.e - v.st > lane_max) continue;
+    if (o.status[r] != TFRG_OK) continue;
+    gather_record<COMPAT>(B, sc, o, r, v);
+  }
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchema sc, DevOut o) {
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  const uint32_t nbig = o.info[kInfoBig];
+  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
+    const uint32_t r = o.big_list[i];
+    if (lane != 0 || o.status[r] != TFRG_OK) continue;
+    const RecView v = rec_view(B, r);
+    gather_record<COMPAT>(B, sc, o, r, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// launcher
+// ------------------------------------------------------------------------------------------------
+constexpr int kLaneRep = 8;  // CRC table bank replication in the lane kernel
+
+template <bool COMPAT>
+static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
+                             const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st) {
+  const size_t lane_lds = 1024ull * kLaneRep * 4 + (size_t)sc.n_slots * kLaneBlock * 2;
+  const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
+  if (lane_lds > 160 * 1024 || wave_lds > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st, b, sc,
+                     o, d_tab, cfg.lane_max);
+  hipLaunchKernelGGL((k_wave_count<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o, d_tab,
+                     d_consts);
+  if (sc.n_slots > 0) {
+    const uint32_t n_tiles = (b.n + kScanTile - 1) / kScanTile;
+    hipLaunchKernelGGL(k_scan, dim3(n_tiles * sc.n_slots), dim3(kScanBlock), 0, st, o.count, o.rs, o.totals,
+                       o.granules, o.ticket, o.info, b.n, n_tiles);
+  }
+  hipLaunchKernelGGL(k_base, dim3(1), dim3(64), 0, st, o.totals, sc.slot_kind, o.slot_base, o.kind_totals,
+                     sc.n_slots);
+  if (sc.n_slots > 0) {
+    hipLaunchKernelGGL((k_lane_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), 0, st, b, sc, o,
+                       cfg.lane_max);
+    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
+                         const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st) {
+  if (b.flags & kFlagSpecVarint) return launch_all<false>(b, sc, o, cfg, d_tab, d_consts, st);
+  return launch_all<true>(b, sc, o, cfg, d_tab, d_consts, st);
+}
+
+}  // namespace tfrg
