@@ -1,0 +1,193 @@
+"""Device path (libtfrg on gfx950) vs the reference: golden vectors and the pinned CPU oracle.
+
+Bit-exact on everything: decoded values (int64, float32 bit patterns, bytes), key order, the
+exception type + message for malformed records, framing offsets and CRC-32C verdicts.
+"""
+
+import struct
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import _golden as G
+from tfr_reader import _status as S
+from tfr_reader import hip, synth
+
+pytestmark = pytest.mark.gpu
+
+KIND = {1: "bytes_list", 2: "float_list", 3: "int64_list"}
+
+
+def raw_entries(r: hip.BatchResult, i: int):
+    """[(key bytes, kind, values)] straight from the columns (float values as raw bits)."""
+    col = r.order[:, i]
+    present = np.flatnonzero(col)
+    present = present[np.argsort(col[present], kind="stable")]
+    out = []
+    for s in present.tolist():
+        lo = int(r.slot_base[s] + r.row_splits[s, i])
+        hi = int(r.slot_base[s] + r.row_splits[s, i + 1])
+        kind = r.slot_kind[s]
+        if kind == 3:
+            vals = r.i64[lo:hi].tolist()
+        elif kind == 2:
+            vals = r.f32[lo:hi].tolist()
+        else:
+            vals = [r.buf[o : o + n].tobytes() for o, n in zip(r.bytes_off[lo:hi].tolist(), r.bytes_len[lo:hi].tolist())]
+        out.append((r.slot_key[s].encode("utf-8"), KIND[kind], vals))
+    return out
+
+
+@pytest.fixture(scope="module")
+def dec():
+    d = hip.HipDecoder(0)
+    yield d
+    d.close()
+
+
+@pytest.fixture(scope="module")
+def orc():
+    return O.Oracle()
+
+
+def payload_batch(payloads):
+    lens = np.array([len(p) for p in payloads], np.uint64)
+    ends = np.cumsum(lens, dtype=np.uint64)
+    return b"".join(payloads), ends - lens, ends
+
+
+@pytest.mark.parametrize("lane_max", [1 << 20, 0])
+def test_golden_cases_bit_exact(dec, lane_max):
+    """Every reference case (valid, malformed, fuzzed) in one device batch; lane_max=0 forces the
+    wavefront-per-record kernels, 1 MiB the lane-per-record kernels."""
+    cases = G.load_cases()
+    payloads = [bytes.fromhex(c["payload"]) for c in cases]
+    dec.set_lane_max(lane_max)
+    try:
+        r = dec.decode(*payload_batch(payloads), payload_only=True)
+    finally:
+        dec.set_lane_max(16384)
+    bad = []
+    for i, c in enumerate(cases):
+        st, aux = int(r.status[i]), int(r.aux[i])
+        ent = raw_entries(r, i) if st == 0 else None
+        err = G.check_against_golden(c["ref"], st, aux, ent, payloads[i])
+        if err:
+            bad.append(f"{c['name']}: {err}")
+    assert not bad, "\n".join(bad[:15])
+
+
+@pytest.mark.parametrize("name", G.FILES)
+def test_golden_files_framed(dec, name):
+    data, meta = G.load_file(name)
+    ptrs = np.array(meta["pointers"], np.uint64).reshape(-1, 3)
+    r = dec.decode(np.frombuffer(data, np.uint8), ptrs[:, 0], ptrs[:, 1])
+    bad = []
+    for i, ref in enumerate(meta["records"]):
+        s, e = int(ptrs[i, 0]), int(ptrs[i, 1])
+        payload = data[s + 12 : e - 4]
+        st = int(r.status[i])
+        err = G.check_against_golden(ref, st, int(r.aux[i]), raw_entries(r, i) if st == 0 else None, payload)
+        if err:
+            bad.append(err)
+        want = meta["crc"][i]
+        got = [int(bool(r.verdict[i] & 2)), int(bool(r.verdict[i] & 4))]
+        if got != want:
+            bad.append(f"record {i}: crc verdict {got} != {want}")
+        if not r.verdict[i] & 1:
+            bad.append(f"record {i}: length field mismatch")
+    assert not bad, bad[:10]
+
+
+def _compare_to_oracle(r, orc, buf, starts, ends, check_crc=True, idx=None):
+    bad = []
+    raw = buf.tobytes()
+    for i in range(len(starts)) if idx is None else idx:
+        s, e = int(starts[i]), int(ends[i])
+        payload = raw[s + 12 : e - 4]
+        st, aux, ent = orc.decode(payload)
+        if int(r.status[i]) != st:
+            bad.append(f"record {i}: status {int(r.status[i])} != oracle {st}")
+            continue
+        if st == 0 and G.canon_entries(raw_entries(r, i)) != G.canon_entries(ent):
+            bad.append(f"record {i}: values differ")
+        if check_crc:
+            lc = O.masked_crc32c(raw[s : s + 8]) == struct.unpack("<I", raw[s + 8 : s + 12])[0]
+            dc = O.masked_crc32c(payload) == struct.unpack("<I", raw[e - 4 : e])[0]
+            if bool(r.verdict[i] & 2) != lc or bool(r.verdict[i] & 4) != dc:
+                bad.append(f"record {i}: crc verdict")
+        if len(bad) > 10:
+            break
+    return bad
+
+
+def test_c1_shape_vs_oracle(dec, orc):
+    buf, st, en = synth.framed(synth.c1_payloads(65536))
+    r = dec.decode(buf, st, en)
+    assert r.info.n_big == 0
+    assert (r.verdict == 7).all()
+    bad = _compare_to_oracle(r, orc, buf, st, en, check_crc=False, idx=range(0, 65536, 7))
+    assert not bad, bad[:10]
+    labels = r.i64[int(r.slot_base[r.slot_key.index("label")]) :][:65536]
+    assert np.array_equal(labels, np.arange(65536) % 1000)
+
+
+def test_c2_shape_vs_oracle(dec, orc):
+    """Large skewed records (wavefront kernels: wave CRC, bytes views)."""
+    buf, st, en = synth.framed(synth.c2_payloads(96, seed=5))
+    # corrupt a few payloads and length CRCs: verdicts must flag them, decode must still succeed
+    b = buf.copy()
+    b[int(st[3]) + 200] ^= 1
+    b[int(st[7]) + 9] ^= 0x80
+    r = dec.decode(b, st, en)
+    assert r.info.n_big > 0
+    assert not _compare_to_oracle(r, orc, b, st, en)
+    assert not r.verdict[3] & 4 and r.verdict[3] & 2
+    assert not r.verdict[7] & 2 and r.verdict[7] & 4
+
+
+def test_c3_shape_vs_oracle(dec, orc):
+    buf, st, en = synth.framed(synth.c3_payloads(512, seed=9))
+    r = dec.decode(buf, st, en)
+    assert not _compare_to_oracle(r, orc, buf, st, en)
+
+
+@pytest.mark.parametrize("lane_max", [0, 1 << 20])
+def test_lane_and_wave_kernels_agree(dec, lane_max):
+    pl = synth.c3_payloads(64, seed=11) + synth.c1_payloads(300) + synth.c2_payloads(8, seed=4, scale=0.1)
+    buf, st, en = synth.framed(pl)
+    base = dec.decode(buf, st, en)
+    dec.set_lane_max(lane_max)
+    try:
+        other = dec.decode(buf, st, en)
+    finally:
+        dec.set_lane_max(16384)
+    for name in ("status", "verdict", "order", "row_splits", "i64", "f32", "bytes_off", "bytes_len"):
+        assert np.array_equal(getattr(base, name), getattr(other, name)), name
+
+
+def test_spec_varint_mode(orc):
+    from tests.golden.gen_golden import entry, example, i64
+
+    vals = [2**31, 2**32, 2**35, -9, -(2**31), 5, 2**63 - 1, -(2**63)]
+    payload = example(entry(b"k", i64(*vals)))
+    d = hip.HipDecoder(0, spec_varint=True)
+    r = d.decode(*payload_batch([payload]), payload_only=True)
+    assert raw_entries(r, 0)[0][2] == vals
+    d.close()
+    r2 = hip.decode_payloads([payload])
+    assert raw_entries(r2, 0)[0][2] == orc.decode(payload)[2][0][2]
+
+
+def test_read_errors_and_truncation(dec):
+    buf, st, en = synth.framed(synth.c1_payloads(4))
+    st = st.copy()
+    en = en.copy()
+    en[3] += 100  # runs past the buffer: clamped, flagged truncated
+    st2 = np.append(st, [buf.size + 5])  # starts past the end: empty read -> OSError
+    en2 = np.append(en, [buf.size + 50])
+    r = dec.decode(buf, st2, en2)
+    assert int(r.status[4]) == S.ERR_READ
+    assert r.verdict[3] & 8
+    assert isinstance(r.error(4), OSError)

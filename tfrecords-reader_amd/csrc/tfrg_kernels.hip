@@ -235,6 +235,9 @@ __device__ int walk_entry(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux
   }
   if (cnt < 2) return TFRG_UB_SHORT_MAP_ENTRY;
   const int kid = sink.lookup(s, f0.off, f0.len);
+  // An unknown key may be invalid UTF-8, which would raise before the feature is parsed: report
+  // it now (kind 0 = key only) so the next round can rank this record's errors correctly.
+  if (kid == -1) sink.note_miss(0, f0.off, f0.len);
   if (kid == -2) {  // interned as invalid UTF-8: bytes(key).decode('utf-8') raises here
     aux = (int64_t)(((uint64_t)f0.off << 32) | (uint64_t)(uint32_t)f0.len);
     return TFRG_ERR_KEY_UTF8;
@@ -302,7 +305,7 @@ struct CountSink {
   bool leader;       // issues global writes and atomics
 
   __device__ __forceinline__ void reset() {
-    for (uint32_t k = 0; k < sc->n_slots; ++k) ord[k * ostride] = 0;
+    for (uint32_t k = 0; k < sc->n_slots; ++k) ord[(size_t)k * ostride] = 0;
     rank = 0;
   }
 
@@ -328,31 +331,35 @@ struct CountSink {
     return -1;
   }
 
+  __device__ void note_miss(int kind, int64_t koff, int64_t klen) {
+    miss = true;
+    if (leader) {
+      const uint32_t i = atomicAdd(&o->info[kInfoMissEntries], 1u);
+      if (i < o->miss_cap) {
+        uint32_t* m = o->miss + 4ull * i;
+        m[0] = r;
+        m[1] = (uint32_t)kind;
+        m[2] = (uint32_t)(p0 + (uint64_t)koff);
+        m[3] = (uint32_t)klen;
+      }
+    }
+  }
+
   __device__ int insert(int kid, int kind, int64_t lo, int64_t ll, uint32_t count, int64_t koff,
                         int64_t klen) {
     const int slot = kid >= 0 ? sc->key_slot[kid * 4 + kind] : -1;
     if (slot < 0) {  // schema miss: report the (key, kind) so the host can intern it
-      miss = true;
-      if (leader) {
-        const uint32_t i = atomicAdd(&o->info[kInfoMissEntries], 1u);
-        if (i < o->miss_cap) {
-          uint32_t* m = o->miss + 4ull * i;
-          m[0] = r;
-          m[1] = (uint32_t)kind;
-          m[2] = (uint32_t)(p0 + (uint64_t)koff);
-          m[3] = (uint32_t)klen;
-        }
-      }
+      note_miss(kind, koff, klen);
       return TFRG_OK;
     }
     uint32_t rk = 0;
     for (int k = 1; k <= 3; ++k) {  // duplicate key (any kind): keep its first position
       const int s2 = sc->key_slot[kid * 4 + k];
       if (s2 >= 0) {
-        const uint32_t v = ord[(uint32_t)s2 * ostride];
+        const uint32_t v = ord[(size_t)s2 * ostride];
         if (v) {
           rk = v;
-          ord[(uint32_t)s2 * ostride] = 0;
+          ord[(size_t)s2 * ostride] = 0;
         }
       }
     }
@@ -360,7 +367,7 @@ struct CountSink {
       if (rank >= 65534u) return TFRG_ST_LIMIT;
       rk = ++rank;
     }
-    ord[(uint32_t)slot * ostride] = (uint16_t)rk;
+    ord[(size_t)slot * ostride] = (uint16_t)rk;
     if (leader) {
       const size_t at = (size_t)slot * n + r;
       o->count[at] = count;
@@ -371,7 +378,7 @@ struct CountSink {
 
   __device__ void finalize(bool ok) {
     for (uint32_t k = 0; k < sc->n_slots; ++k) {
-      const uint32_t v = ok ? ord[k * ostride] : 0u;
+      const uint32_t v = ok ? ord[(size_t)k * ostride] : 0u;
       if (leader) {
         const size_t at = (size_t)k * n + r;
         o->order[at] = (uint16_t)v;
@@ -538,7 +545,9 @@ __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int s
   }
 }
 
-template <int R, bool COMPAT>
+// GORD: keep the per-record dict state in the global `order` column instead of LDS (key tables too
+// large for LDS); same results, slower.
+template <int R, bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            uint32_t lane_max) {
@@ -561,7 +570,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
       continue;
     }
     int64_t aux = 0;
-    CountSink sink{&sc, &o, ord + threadIdx.x, kLaneBlock, 0, B.n, r, v.p0, false, true};
+    CountSink sink{&sc, &o, GORD ? o.order + r : ord + threadIdx.x, GORD ? B.n : (uint32_t)kLaneBlock, 0,
+                   B.n, r, v.p0, false, true};
     int status = v.status;
     if (status == TFRG_OK) {
       if (framed) {
@@ -579,7 +589,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
           }
         }
       }
-      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[k * kLaneBlock] = 0;
+      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
       Src s;
       s.init(B.bytes, v.p0, v.L);
       status = walk_example<COMPAT>(s, sink, aux);
@@ -590,7 +600,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
   }
 }
 
-template <bool COMPAT>
+template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
                                                           const uint32_t* __restrict__ crc_tab,
                                                           const uint32_t* __restrict__ consts) {
@@ -611,7 +621,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
     const uint32_t r = o.big_list[i];
     RecView v = rec_view(B, r);
     int64_t aux = 0;
-    CountSink sink{&sc, &o, word, 1, 0, B.n, r, v.p0, false, lane == 0};
+    CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
     if (framed) {
       const uint64_t D = v.e - v.st;
       if (D >= 8) {
@@ -629,7 +639,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
         }
       }
     }
-    for (uint32_t k = lane; k < sc.n_slots; k += 64) word[k] = 0;
+    for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
     __builtin_amdgcn_wave_barrier();
     Src s;
     s.init(B.bytes, v.p0, v.L);
@@ -820,16 +830,28 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchem
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneRep = 8;  // CRC table bank replication in the lane kernel
 
+constexpr size_t kLdsBudget = 96 * 1024;  // above this the dict state goes to the global column
+
 template <bool COMPAT>
 static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
                              const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st) {
-  const size_t lane_lds = 1024ull * kLaneRep * 4 + (size_t)sc.n_slots * kLaneBlock * 2;
+  const size_t tab_lds = 1024ull * kLaneRep * 4;
+  const size_t lane_lds = tab_lds + (size_t)sc.n_slots * kLaneBlock * 2;
   const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
-  if (lane_lds > 160 * 1024 || wave_lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st, b, sc,
-                     o, d_tab, cfg.lane_max);
-  hipLaunchKernelGGL((k_wave_count<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o, d_tab,
-                     d_consts);
+  if (lane_lds <= kLdsBudget) {
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
+                       b, sc, o, d_tab, cfg.lane_max);
+  } else {
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), tab_lds, st, b,
+                       sc, o, d_tab, cfg.lane_max);
+  }
+  if (wave_lds <= kLdsBudget) {
+    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o,
+                       d_tab, d_consts);
+  } else {
+    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b, sc,
+                       o, d_tab, d_consts);
+  }
   if (sc.n_slots > 0) {
     const uint32_t n_tiles = (b.n + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan, dim3(n_tiles * sc.n_slots), dim3(kScanBlock), 0, st, o.count, o.rs, o.totals,

@@ -42,7 +42,8 @@ class KeyTable:
         self.version = 0
 
     def intern(self, key: bytes, kind: int) -> bool:
-        """Add key (and its (key, kind) slot when the key is valid UTF-8). True if anything new."""
+        """Add key (and its (key, kind) slot when kind != 0 and the key is valid UTF-8).
+        Returns True if anything new was added."""
         new = False
         kid = self.key_ids.get(key)
         if kid is None:
@@ -54,7 +55,7 @@ class KeyTable:
             except UnicodeDecodeError:
                 self.key_str.append(None)
             new = True
-        if self.key_str[kid] is not None and (kid, kind) not in self.slots:
+        if kind and self.key_str[kid] is not None and (kid, kind) not in self.slots:
             self.slots[(kid, kind)] = len(self.slot_key)
             self.slot_key.append(kid)
             self.slot_kind.append(kind)
