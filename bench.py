@@ -1,0 +1,249 @@
+#!/usr/bin/env python3
+"""Device-resident TFRecord -> tf.train.Example -> Feature decode throughput on MI355X.
+
+Workload (BASELINE.json configs[1], C1, scaled for a rate measurement as SURVEY §8d D3 asks): per
+GPU one resident batch of 256 files x 65,536 C1-shaped records (int64 label + 12-byte bytes_list
+id, ~59 B framed, spec CRC-32C) = 16,777,216 records, ~0.92 GiB. A step is one full decode of that
+batch: framing check + masked CRC-32C of length and payload + reference-exact Example decode +
+columnar gather of every value (k_lane_count .. k_wave_gather), inputs already in HBM. At N GPUs
+every rank decodes its own 256-file shard (weak scaling, no collective on the data path; the
+barrier and the max-over-ranks timing use RCCL).
+
+Prints ONE JSON line (rank 0). ``roofline`` is for the dominant kernel, timed with HIP events on
+the stream the kernels run on; ``cpu_baseline`` is the oracle (the C restatement of the reference
+decoder) on host threads over a bounded sample of the same records.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+for p in (str(REPO / "tfrecords-reader_amd"), str(REPO)):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, 8.0 TB/s (MI355X_MICROARCH.md, chip-level parameters)
+RECORDS_PER_FILE = 65536
+FILES_PER_GPU = 256
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--files", type=int, default=FILES_PER_GPU, help="C1 files (x65,536 records) per GPU")
+    ap.add_argument("--profile-steps", type=int, default=5)
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
+    ap.add_argument("--no-cpu", action="store_true")
+    return ap.parse_args()
+
+
+def build_shard(rank: int, files: int):
+    """Framed C1 image of one file (seeded by rank) replicated `files` times."""
+    from tfr_reader import synth
+
+    pl = synth.c1_payloads(RECORDS_PER_FILE, offset=rank * RECORDS_PER_FILE)
+    buf, st, en = synth.framed(pl, crc=True)
+    return (buf, st, en), synth.replicate(buf, st, en, files)
+
+
+def cpu_baseline(sample, seconds: float) -> dict:
+    """Oracle decode (restated reference algorithm, C) of the sample on host threads."""
+    from oracle import oracle as O
+
+    buf, st, en = sample
+    O.lib()
+    cores = min(16, len(os.sched_getaffinity(0)))
+    nbytes = int((en - st).sum())
+
+    def work(_):
+        done_b = done_r = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < seconds:
+            status, _ = O.decode_framed_bulk(buf, st, en)
+            assert not status.any()
+            done_b += nbytes
+            done_r += st.shape[0]
+        return done_b, done_r
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(cores) as ex:
+        res = list(ex.map(work, range(cores)))
+    wall = time.perf_counter() - t0
+    b = sum(r[0] for r in res)
+    r = sum(r[1] for r in res)
+    return {
+        "value": b / wall / 2**30,
+        "unit": "GiB/s",
+        "examples_per_s": r / wall,
+        "cores": cores,
+        "kind": "port",
+        "sample": f"one C1 file ({st.shape[0]} records, {nbytes / 2**20:.2f} MiB) decoded repeatedly by "
+        f"{cores} threads for {seconds:.1f} s wall ({cores * seconds:.0f} core-s)",
+    }
+
+
+def main() -> None:
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+
+    from tfr_reader import hip
+
+    sample, (big, st, en) = build_shard(rank, args.files)
+    n = int(st.shape[0])
+    nbytes = int(big.size)
+    framed_bytes = int((en - st).sum())
+    dev = torch.device("cuda", local)
+    d_bytes = torch.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
+    d_bytes[:nbytes].copy_(torch.from_numpy(big))
+    d_st = torch.from_numpy(st.view(np.int64)).to(dev)
+    d_en = torch.from_numpy(en.view(np.int64)).to(dev)
+    del big
+    stream = torch.cuda.current_stream(dev)
+
+    dec = hip.HipDecoder(local)
+    dec.decode(*sample)  # learns the key table (host path, schema-miss rounds)
+
+    def step():
+        dec.decode_device(d_bytes.data_ptr(), nbytes, d_st.data_ptr(), d_en.data_ptr(), n, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    info = dec.info()
+    assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0, "decode check failed"
+    assert info.kind_totals[3] == n and info.kind_totals[1] == n, "value totals"
+
+    # ---- timed region
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize(dev)
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(stream)
+    for _ in range(args.steps):
+        step()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    wall = time.perf_counter() - t0
+    if dist:
+        tdist.barrier()
+    ev_s = e0.elapsed_time(e1) / 1e3
+    elapsed = max(wall, ev_s)
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    info = dec.info()
+    assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0
+
+    # ---- per-kernel durations (HIP events on the launch stream), for the roofline
+    dec.set_profiling(True)
+    per: dict[str, list[float]] = {}
+    for _ in range(args.profile_steps):
+        step()
+        for k, v in dec.profile_last().items():
+            per.setdefault(k, []).append(v)
+    dec.set_profiling(False)
+    kern_ms = {k: float(np.mean(v)) for k, v in per.items()}
+    dominant = max(kern_ms, key=kern_ms.get)
+
+    # algorithmic bytes: k_lane_count reads every framed byte plus the two
+    # u64 offsets and writes the u32 status of each record.
+    alg = {
+        "k_lane_count": framed_bytes + 16 * n + 4 * n,
+        # k_lane_gather re-reads each present list and writes the values: label int64 (8 B) and
+        # the id view (8 B), reading order/loc/row-splits of both slots (2 x (2+8+4) B)
+        "k_lane_gather": n * (2 * 14 + 8 + 8),
+    }
+    a_bytes = alg.get(dominant, framed_bytes + 20 * n)
+    achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
+    # whole-pipeline algorithmic bytes: R + W
+    n_keys = 2
+    R = framed_bytes + 16 * n
+    W = 4 * n + 4 * n * n_keys + 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 12 * int(info.kind_totals[1])
+
+    ms_step = elapsed / args.steps * 1e3
+    gib_s_rank = framed_bytes / (ms_step / 1e3) / 2**30
+    value = framed_bytes * world / (elapsed / args.steps) / 2**30
+    ex_s = n * world / (elapsed / args.steps)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(sample, args.cpu_seconds)
+
+    if dist:
+        tdist.barrier()
+    if rank == 0:
+        metric = json.loads((REPO / "BASELINE.json").read_text())["metric"]
+        line = {
+            "metric": metric,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "examples_per_s": round(ex_s, 1),
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": f"C1 (configs[1]): {args.files} files x {RECORDS_PER_FILE} records per GPU, "
+                "int64 label + 12 B bytes_list id, spec CRC-32C, resident in HBM",
+                "records_per_gpu": n,
+                "framed_bytes_per_gpu": framed_bytes,
+                "parallelism": f"file-sharded x{world} (no collective on the data path)",
+                "per_gpu_GiB_s": round(gib_s_rank, 3),
+            },
+            "kernels_ms": {k: round(v, 4) for k, v in kern_ms.items()},
+            "roofline": {
+                "kernel": dominant,
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": PEAK_HBM_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / PEAK_HBM_GBS, 4),
+                "traffic": None,
+                "algorithmic_bytes_per_launch": a_bytes,
+            },
+            "pipeline": {
+                "alg_bytes_R_plus_W": R + W,
+                "achieved_GBps": round((R + W) / (ms_step / 1e3) / 1e9, 1),
+                "frac": round((R + W) / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    dec.close()
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

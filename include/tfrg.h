@@ -71,6 +71,12 @@ int tfrg_ctx_destroy(tfrg_ctx* ctx);
 /* records larger than lane_max bytes take the wavefront-per-record kernels (default 16384) */
 int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
 
+/* Per-kernel timing: with profiling on, every decode records HIP events on its stream around
+ * each kernel stage; tfrg_profile_last waits for the last decode and writes up to cap stage
+ * durations (ms) and names, returning the stage count. */
+int tfrg_ctx_set_profiling(tfrg_ctx* ctx, int on);
+int tfrg_profile_last(tfrg_ctx* ctx, float* ms, const char** names, int cap);
+
 /* Key table ("schema"): n_keys distinct key byte strings (key_blob[key_offsets[i]..[i+1]]),
  * key_flags bit0 = the bytes are not valid UTF-8 (decoder.pyx:164 would raise); n_slots columns,
  * slot s = (slot_key[s], slot_kind[s]) with kind 1 bytes_list, 2 float_list, 3 int64_list.

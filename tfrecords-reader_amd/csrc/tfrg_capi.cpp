@@ -78,6 +78,10 @@ struct tfrg_ctx {
   uint64_t nbytes = 0;
   uint64_t cap_i64 = 0, cap_f32 = 0, cap_b = 0;
   bool have_result = false;
+  // optional per-stage HIP events (tfrg_ctx_set_profiling)
+  bool profiling = false;
+  bool have_events = false;
+  hipEvent_t ev[kNumStages + 1] = {};
 };
 
 extern "C" {
@@ -131,6 +135,8 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->granules, &c->ticket};
   for (DBuf* b : all) b->release();
+  if (c->have_events)
+    for (auto& e : c->ev) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
   delete c;
   return 0;
@@ -140,6 +146,25 @@ int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
   if (!c) return TFRG_E_ARG;
   c->lane_max = lane_max;
   return 0;
+}
+
+int tfrg_ctx_set_profiling(tfrg_ctx* c, int on) {
+  if (!c) return TFRG_E_ARG;
+  c->profiling = on != 0;
+  return 0;
+}
+
+int tfrg_profile_last(tfrg_ctx* c, float* ms, const char** names, int cap) {
+  if (!c || !c->have_events || !c->have_result) return TFRG_E_ARG;
+  HIP_TRY(hipEventSynchronize(c->ev[kNumStages]));
+  const int k = cap < kNumStages ? cap : (int)kNumStages;
+  for (int i = 0; i < k; ++i) {
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, c->ev[i], c->ev[i + 1]));
+    if (ms) ms[i] = t;
+    if (names) names[i] = kStageNames[i];
+  }
+  return k;
 }
 
 static uint32_t fnv1a(const uint8_t* p, uint64_t n) {
@@ -291,7 +316,15 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
   cfg.lane_max = c->lane_max;
   if (n) {
-    hipError_t e = launch_decode(b, schema_view(c), o, cfg, c->crc_tab.as<uint32_t>(), c->consts.as<uint32_t>(), st);
+    hipEvent_t* ev = nullptr;
+    if (c->profiling) {
+      if (!c->have_events) {
+        for (auto& e : c->ev) HIP_TRY(hipEventCreate(&e));
+        c->have_events = true;
+      }
+      ev = c->ev;
+    }
+    hipError_t e = launch_decode(b, schema_view(c), o, cfg, c->crc_tab.as<uint32_t>(), c->consts.as<uint32_t>(), st, ev);
     if (e != hipSuccess) {
       set_error(std::string("kernel launch: ") + hipGetErrorString(e));
       return TFRG_E_HIP;

@@ -80,7 +80,14 @@ struct LaunchCfg {
   uint32_t lane_max;       // records above this size go to the wave kernels
 };
 
+// Kernel stages, in launch order (profiling events bracket each one).
+enum Stage : int { kStageLaneCount = 0, kStageWaveCount, kStageScan, kStageBase, kStageLaneGather, kStageWaveGather,
+                   kNumStages };
+extern const char* const kStageNames[kNumStages];
+
+// ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.
 hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
-                         const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream);
+                         const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream,
+                         hipEvent_t* ev);
 
 }  // namespace tfrg

@@ -832,12 +832,19 @@ constexpr int kLaneRep = 8;  // CRC table bank replication in the lane kernel
 
 constexpr size_t kLdsBudget = 96 * 1024;  // above this the dict state goes to the global column
 
+const char* const kStageNames[kNumStages] = {"k_lane_count", "k_wave_count", "k_scan",
+                                             "k_base",       "k_lane_gather", "k_wave_gather"};
+
 template <bool COMPAT>
 static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
-                             const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st) {
+                             const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st, hipEvent_t* ev) {
+  auto mark = [&](int i) {
+    if (ev) (void)hipEventRecord(ev[i], st);
+  };
   const size_t tab_lds = 1024ull * kLaneRep * 4;
   const size_t lane_lds = tab_lds + (size_t)sc.n_slots * kLaneBlock * 2;
   const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
+  mark(kStageLaneCount);
   if (lane_lds <= kLdsBudget) {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
                        b, sc, o, d_tab, cfg.lane_max);
@@ -845,6 +852,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), tab_lds, st, b,
                        sc, o, d_tab, cfg.lane_max);
   }
+  mark(kStageWaveCount);
   if (wave_lds <= kLdsBudget) {
     hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o,
                        d_tab, d_consts);
@@ -852,25 +860,32 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b, sc,
                        o, d_tab, d_consts);
   }
+  mark(kStageScan);
   if (sc.n_slots > 0) {
     const uint32_t n_tiles = (b.n + kScanTile - 1) / kScanTile;
     hipLaunchKernelGGL(k_scan, dim3(n_tiles * sc.n_slots), dim3(kScanBlock), 0, st, o.count, o.rs, o.totals,
                        o.granules, o.ticket, o.info, b.n, n_tiles);
   }
+  mark(kStageBase);
   hipLaunchKernelGGL(k_base, dim3(1), dim3(64), 0, st, o.totals, sc.slot_kind, o.slot_base, o.kind_totals,
                      sc.n_slots);
+  mark(kStageLaneGather);
   if (sc.n_slots > 0) {
     hipLaunchKernelGGL((k_lane_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), 0, st, b, sc, o,
                        cfg.lane_max);
+  }
+  mark(kStageWaveGather);
+  if (sc.n_slots > 0) {
     hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
   }
+  mark(kNumStages);
   return hipGetLastError();
 }
 
 hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
-                         const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st) {
-  if (b.flags & kFlagSpecVarint) return launch_all<false>(b, sc, o, cfg, d_tab, d_consts, st);
-  return launch_all<true>(b, sc, o, cfg, d_tab, d_consts, st);
+                         const uint32_t* d_tab, const uint32_t* d_consts, hipStream_t st, hipEvent_t* ev) {
+  if (b.flags & kFlagSpecVarint) return launch_all<false>(b, sc, o, cfg, d_tab, d_consts, st, ev);
+  return launch_all<true>(b, sc, o, cfg, d_tab, d_consts, st, ev);
 }
 
 }  // namespace tfrg

@@ -95,6 +95,18 @@ class HipDecoder:
     def set_lane_max(self, nbytes: int) -> None:
         N.check(self._lib.tfrg_ctx_set_lane_max(self._ctx, nbytes), "tfrg_ctx_set_lane_max")
 
+    def set_profiling(self, on: bool) -> None:
+        N.check(self._lib.tfrg_ctx_set_profiling(self._ctx, int(on)), "tfrg_ctx_set_profiling")
+
+    def profile_last(self) -> dict[str, float]:
+        """Per-kernel durations (ms) of the last decode (needs set_profiling(True) before it)."""
+        ms = (C.c_float * 16)()
+        names = (C.c_char_p * 16)()
+        k = self._lib.tfrg_profile_last(self._ctx, ms, names, 16)
+        if k < 0:
+            N.check(k, "tfrg_profile_last")
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
     # ------------------------------------------------------------------ schema
     def push_schema(self) -> None:
         kt = self.keys
