@@ -68,10 +68,37 @@ struct Src {
   }
 };
 
+// The same payload view over a wave's LDS stage: lds[0] holds absolute byte `lo`.
+struct LdsSrc {
+  const uint8_t* lds;
+  uint64_t lo;
+  uint64_t p0;
+  int64_t L;
+  bool ub;
+
+  __device__ __forceinline__ void init(const uint8_t* l, uint64_t lo_, uint64_t p, int64_t len) {
+    lds = l;
+    lo = lo_;
+    p0 = p;
+    L = len;
+    ub = false;
+  }
+  __device__ __forceinline__ uint32_t at(int64_t i) {
+    if (i >= L) {
+      ub |= (i > L);
+      return 0u;
+    }
+    return lds[(uint32_t)(p0 - lo) + (uint32_t)i];
+  }
+  __device__ __forceinline__ uint32_t u32(int64_t i) {
+    return at(i) | (at(i + 1) << 8) | (at(i + 2) << 16) | (at(i + 3) << 24);
+  }
+};
+
 // decode_varint (decoder.pyx:34-50). COMPAT reproduces the reference's int-width shift:
 // term = (int32)((b & 0x7F) << (shift & 31)), sign-extended.
-template <bool COMPAT>
-__device__ __forceinline__ int rd_varint(Src& s, int64_t& pos, int64_t& val) {
+template <bool COMPAT, class S>
+__device__ __forceinline__ int rd_varint(S& s, int64_t& pos, int64_t& val) {
   int64_t r = 0;
   int shift = 0;
   for (;;) {
@@ -93,7 +120,8 @@ __device__ __forceinline__ int rd_varint(Src& s, int64_t& pos, int64_t& val) {
 }
 
 // same control flow without assembling the value (counting passes)
-__device__ __forceinline__ int skip_varint(Src& s, int64_t& pos) {
+template <class S>
+__device__ __forceinline__ int skip_varint(S& s, int64_t& pos) {
   int shift = 0;
   for (;;) {
     const uint32_t b = s.at(pos);
@@ -110,8 +138,8 @@ struct Fld {
 };
 
 // One iteration of decode_message (decoder.pyx:69-104).
-template <bool COMPAT>
-__device__ __forceinline__ int rd_field(Src& s, int64_t& pos, int64_t end, Fld& f, int64_t& aux) {
+template <bool COMPAT, class S>
+__device__ __forceinline__ int rd_field(S& s, int64_t& pos, int64_t end, Fld& f, int64_t& aux) {
   int64_t key;
   int st = rd_varint<COMPAT>(s, pos, key);
   if (st) return st;
@@ -152,8 +180,8 @@ __device__ __forceinline__ int rd_field(Src& s, int64_t& pos, int64_t end, Fld& 
 
 // decode_message validation pass: every tag/length of one level before any child is parsed,
 // which is the reference's level-by-level error precedence.
-template <bool COMPAT>
-__device__ int scan_msg(Src& s, int64_t pos, int64_t end, int64_t& aux) {
+template <bool COMPAT, class S>
+__device__ int scan_msg(S& s, int64_t pos, int64_t end, int64_t& aux) {
   Fld f;
   while (pos < end) {
     const int st = rd_field<COMPAT>(s, pos, end, f, aux);
@@ -163,8 +191,8 @@ __device__ int scan_msg(Src& s, int64_t pos, int64_t end, int64_t& aux) {
 }
 
 // bytes/float/int64 list (decoder.pyx:203-300): validation + element count.
-template <bool COMPAT>
-__device__ int list_count(Src& s, int kind, int64_t o, int64_t n, int64_t& aux, uint32_t& count) {
+template <bool COMPAT, class S>
+__device__ int list_count(S& s, int kind, int64_t o, int64_t n, int64_t& aux, uint32_t& count) {
   const int64_t end = o + n;
   int st = scan_msg<COMPAT>(s, o, end, aux);
   if (st) return st;
@@ -198,8 +226,8 @@ __device__ int list_count(Src& s, int kind, int64_t o, int64_t n, int64_t& aux, 
 }
 
 // feature_from_bytes (decoder.pyx:169-199): kind = field number of the FIRST field.
-template <bool COMPAT>
-__device__ int walk_feature(Src& s, int64_t o, int64_t n, int64_t& aux, int& kind, int64_t& lo,
+template <bool COMPAT, class S>
+__device__ int walk_feature(S& s, int64_t o, int64_t n, int64_t& aux, int& kind, int64_t& lo,
                             int64_t& ll, uint32_t& count) {
   const int64_t end = o + n;
   int64_t pos = o;
@@ -220,8 +248,8 @@ __device__ int walk_feature(Src& s, int64_t o, int64_t n, int64_t& aux, int& kin
 }
 
 // parse_map_entry (decoder.pyx:153-166): positional fields[0] = key, fields[1] = value.
-template <bool COMPAT, class Sink>
-__device__ int walk_entry(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
+template <bool COMPAT, class S, class Sink>
+__device__ int walk_entry(S& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
   const int64_t end = o + n;
   int64_t pos = o;
   Fld f, f0, f1;
@@ -251,8 +279,8 @@ __device__ int walk_entry(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux
 }
 
 // features_from_bytes (decoder.pyx:130-150)
-template <bool COMPAT, class Sink>
-__device__ int walk_features(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
+template <bool COMPAT, class S, class Sink>
+__device__ int walk_features(S& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
   const int64_t end = o + n;
   int st = scan_msg<COMPAT>(s, o, end, aux);
   if (st) return st;
@@ -270,8 +298,8 @@ __device__ int walk_features(Src& s, Sink& sink, int64_t o, int64_t n, int64_t& 
 }
 
 // example_from_bytes (decoder.pyx:107-127) + Feature(proto.features.feature) (feature.py:106)
-template <bool COMPAT, class Sink>
-__device__ int walk_example(Src& s, Sink& sink, int64_t& aux) {
+template <bool COMPAT, class S, class Sink>
+__device__ int walk_example(S& s, Sink& sink, int64_t& aux) {
   const int64_t L = s.L;
   int st = scan_msg<COMPAT>(s, 0, L, aux);
   if (st) return st;
@@ -310,7 +338,8 @@ struct CountSink {
   }
 
   // key bytes -> key id; -1 unknown, -2 interned as invalid UTF-8
-  __device__ int lookup(Src& s, int64_t off, int64_t len) {
+  template <class S>
+  __device__ int lookup(S& s, int64_t off, int64_t len) {
     uint32_t h = 2166136261u;
     for (int64_t i = 0; i < len; ++i) h = (h ^ s.at(off + i)) * 16777619u;
     if (sc->n_keys == 0) return -1;
@@ -545,6 +574,134 @@ __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int s
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wave staging for the lane-per-record kernels: the 64 records of a wave are (in the common case of
+// whole-file batches) one contiguous span of a few KiB. The wave copies that span into its LDS stage
+// with coalesced 16-byte loads (1 KiB per wave-instruction) and every lane then parses its record
+// from LDS instead of issuing scattered, latency-bound global loads.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kStageBytes = 4096;                // span capacity per wave
+constexpr uint32_t kStageStride = kStageBytes + 64;   // + slack for aligned over-reads at the tail
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t y = __shfl_xor(x, m, 64);
+    x = y < x ? y : x;
+  }
+  return x;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    const uint64_t y = __shfl_xor(x, m, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+// LDS writes of one wave made visible to its other lanes
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// copy absolute bytes [lo16, hi) (lo16 16-aligned, hi - lo16 <= kStageBytes) into dst
+__device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
+                                           uint32_t lane) {
+  // four 1 KiB wave-loads in flight per round, held in named registers (no scratch)
+  for (uint32_t off = lane * 16u; lo16 + off < hi; off += 4096u) {
+    const uint64_t q = lo16 + off;
+    const bool h1 = q + 1024 < hi, h2 = q + 2048 < hi, h3 = q + 3072 < hi;
+    const uint4 a = *reinterpret_cast<const uint4*>(src + q);
+    uint4 b = a, c = a, d = a;
+    if (h1) b = *reinterpret_cast<const uint4*>(src + q + 1024);
+    if (h2) c = *reinterpret_cast<const uint4*>(src + q + 2048);
+    if (h3) d = *reinterpret_cast<const uint4*>(src + q + 3072);
+    *reinterpret_cast<uint4*>(dst + off) = a;
+    if (h1) *reinterpret_cast<uint4*>(dst + off + 1024) = b;
+    if (h2) *reinterpret_cast<uint4*>(dst + off + 2048) = c;
+    if (h3) *reinterpret_cast<uint4*>(dst + off + 3072) = d;
+  }
+}
+
+// 4 unaligned bytes at stage offset `off` (two aligned LDS dwords + a byte funnel shift)
+__device__ __forceinline__ uint32_t lds_u32u(const uint8_t* l, uint32_t off) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
+  const uint32_t a = off >> 2, sh = off & 3u;
+  const uint32_t lo = w[a];
+  return sh ? __builtin_amdgcn_alignbyte(w[a + 1], lo, sh) : lo;  // shift in bytes
+}
+
+// CRC-32C of stage bytes [a, b): byte steps to 4-alignment, slice-by-4 words, byte tail
+template <int R>
+__device__ uint32_t crc_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<R>& T) {
+  uint32_t c = 0xffffffffu;
+  while (a < b && (a & 3u)) c = T.step1(c, l[a++]);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
+  for (; a + 4 <= b; a += 4) c = T.step4(c ^ w[a >> 2]);
+  while (a < b) c = T.step1(c, l[a++]);
+  return ~c;
+}
+
+// Framing verdicts + reference walk of one record (lane-per-record), from the stage or from HBM.
+template <int R, bool COMPAT, bool STAGED>
+__device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc, uint32_t r, RecView& v,
+                                         CountSink& sink, const LdsTab<R>& T, const uint8_t* stage, uint64_t lo16,
+                                         int64_t& aux) {
+  const bool framed = !(B.flags & kFlagPayloadOnly);
+  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
+  if (framed) {
+    const uint64_t D = v.e - v.st;
+    if (D >= 8) {
+      uint64_t lenf;
+      if constexpr (STAGED) {
+        const uint32_t o0 = (uint32_t)(v.st - lo16);
+        lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
+      } else {
+        lenf = load_u64_unaligned(B.bytes, v.st);
+      }
+      if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+      if (do_crc && D >= 12) {
+        uint32_t c, stored;
+        if constexpr (STAGED) {
+          c = crc_lds<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
+          stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
+        } else {
+          c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
+          stored = load_u32_unaligned(B.bytes, v.st + 8);
+        }
+        if (crc_mask(c) == stored) v.verdict |= TFRG_V_LEN_CRC;
+      }
+      if (do_crc && D >= 16) {
+        uint32_t c, stored;
+        if constexpr (STAGED) {
+          c = crc_lds<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+          stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
+        } else {
+          c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
+          stored = load_u32_unaligned(B.bytes, v.e - 4);
+        }
+        if (crc_mask(c) == stored) v.verdict |= TFRG_V_DATA_CRC;
+      }
+    }
+  }
+  for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+  int status;
+  if constexpr (STAGED) {
+    LdsSrc s;
+    s.init(stage, lo16, v.p0, v.L);
+    status = walk_example<COMPAT>(s, sink, aux);
+  } else {
+    Src s;
+    s.init(B.bytes, v.p0, v.L);
+    status = walk_example<COMPAT>(s, sink, aux);
+  }
+  if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+  return status;
+}
+
 // GORD: keep the per-record dict state in the global `order` column instead of LDS (key tables too
 // large for LDS); same results, slower.
 template <int R, bool COMPAT, bool GORD>
@@ -554,49 +711,52 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;                                           // 1024 * R dwords
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 1024 * R);   // [n_slots][kLaneBlock]
+  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * kLaneBlock * 2u + 15u) & ~15u);
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds + 1024 * R) + ord_bytes + wib * kStageStride;
   for (uint32_t i = threadIdx.x; i < 1024u * R; i += kLaneBlock) tab[i] = crc_tab[i / R];
   __syncthreads();
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
-  const bool framed = !(B.flags & kFlagPayloadOnly);
-  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
 
-  for (uint64_t ri = (uint64_t)blockIdx.x * kLaneBlock + threadIdx.x; ri < B.n;
-       ri += (uint64_t)gridDim.x * kLaneBlock) {
+  for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
+       base += (uint64_t)gridDim.x * kLaneBlock) {
+    const uint64_t ri = base + lane;
+    const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
-    RecView v = rec_view(B, r);
-    if (v.status == TFRG_OK && v.e - v.st > lane_max) {  // large record: wave kernel
-      const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
-      o.big_list[i] = r;
-      continue;
-    }
-    int64_t aux = 0;
-    CountSink sink{&sc, &o, GORD ? o.order + r : ord + threadIdx.x, GORD ? B.n : (uint32_t)kLaneBlock, 0,
-                   B.n, r, v.p0, false, true};
-    int status = v.status;
-    if (status == TFRG_OK) {
-      if (framed) {
-        const uint64_t D = v.e - v.st;
-        if (D >= 8) {
-          const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
-          if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
-          if (do_crc && D >= 12) {
-            const uint32_t c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
-            if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
-          }
-          if (do_crc && D >= 16) {
-            const uint32_t c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
-            if (crc_mask(c) == load_u32_unaligned(B.bytes, v.e - 4)) v.verdict |= TFRG_V_DATA_CRC;
-          }
-        }
+    RecView v;
+    bool mine = false;
+    if (valid) {
+      v = rec_view(B, r);
+      const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
+      if (big) {  // large record: wavefront kernel
+        const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
+        o.big_list[i] = r;
       }
-      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
-      Src s;
-      s.init(B.bytes, v.p0, v.L);
-      status = walk_example<COMPAT>(s, sink, aux);
-      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+      mine = !big;
     }
-    sink.finalize(status == TFRG_OK);
-    record_result(o, r, status, aux, v.verdict);
+    // wave-uniform staging decision over the span of this wave's records
+    const bool span_rec = mine && v.status == TFRG_OK;
+    const uint64_t lo = wave_min_u64(span_rec ? v.st : ~0ull);
+    const uint64_t hi = wave_max_u64(span_rec ? v.e : 0ull);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = hi > lo && hi - lo16 <= kStageBytes;
+    if (staged) {
+      stage_span(stage, B.bytes, lo16, hi, lane);
+      wave_lds_sync();
+    }
+    if (mine) {
+      int64_t aux = 0;
+      CountSink sink{&sc, &o, GORD ? o.order + r : ord + threadIdx.x, GORD ? B.n : (uint32_t)kLaneBlock, 0,
+                     B.n, r, v.p0, false, true};
+      int status = v.status;
+      if (status == TFRG_OK) {
+        status = staged ? count_one<R, COMPAT, true>(B, sc, r, v, sink, T, stage, lo16, aux)
+                        : count_one<R, COMPAT, false>(B, sc, r, v, sink, T, stage, lo16, aux);
+      }
+      sink.finalize(status == TFRG_OK);
+      record_result(o, r, status, aux, v.verdict);
+    }
+    wave_lds_sync();  // the stage is rewritten by the next iteration
   }
 }
 
@@ -753,8 +913,8 @@ __global__ void k_base(const uint32_t* totals, const uint8_t* slot_kind, uint64_
 // ------------------------------------------------------------------------------------------------
 // Gather: decode the (validated) list message of every present slot into its column.
 // ------------------------------------------------------------------------------------------------
-template <bool COMPAT>
-__device__ void list_gather(Src& s, const DevOut& o, int kind, int64_t lo, int64_t ll, uint64_t dst) {
+template <bool COMPAT, class S>
+__device__ void list_gather(S& s, const DevOut& o, int kind, int64_t lo, int64_t ll, uint64_t dst) {
   const int64_t end = lo + ll;
   int64_t pos = lo, aux = 0;
   Fld f;
@@ -786,11 +946,9 @@ __device__ void list_gather(Src& s, const DevOut& o, int kind, int64_t lo, int64
   }
 }
 
-template <bool COMPAT>
-__device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o,
-                                              uint32_t r, const RecView& v) {
-  Src s;
-  s.init(B.bytes, v.p0, v.L);
+template <bool COMPAT, class S>
+__device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t r,
+                                              S& s) {
   for (uint32_t k = 0; k < sc.n_slots; ++k) {
     const size_t at = (size_t)k * B.n + r;
     if (!o.order[at]) continue;
@@ -803,13 +961,39 @@ __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema
 template <bool COMPAT>
 __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchema sc, DevOut o,
                                                             uint32_t lane_max) {
-  for (uint64_t ri = (uint64_t)blockIdx.x * kLaneBlock + threadIdx.x; ri < B.n;
-       ri += (uint64_t)gridDim.x * kLaneBlock) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kStageStride;
+  for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
+       base += (uint64_t)gridDim.x * kLaneBlock) {
+    const uint64_t ri = base + lane;
     const uint32_t r = (uint32_t)ri;
-    const RecView v = rec_view(B, r);
-    if (v.status != TFRG_OK || v.e - v.st > lane_max) continue;
-    if (o.status[r] != TFRG_OK) continue;
-    gather_record<COMPAT>(B, sc, o, r, v);
+    RecView v;
+    bool mine = false;
+    if (ri < B.n) {
+      v = rec_view(B, r);
+      mine = v.status == TFRG_OK && v.e - v.st <= lane_max && o.status[r] == TFRG_OK;
+    }
+    const uint64_t lo = wave_min_u64(mine ? v.st : ~0ull);
+    const uint64_t hi = wave_max_u64(mine ? v.e : 0ull);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = hi > lo && hi - lo16 <= kStageBytes;
+    if (staged) {
+      stage_span(stage, B.bytes, lo16, hi, lane);
+      wave_lds_sync();
+    }
+    if (mine) {
+      if (staged) {
+        LdsSrc s;
+        s.init(stage, lo16, v.p0, v.L);
+        gather_record<COMPAT>(B, sc, o, r, s);
+      } else {
+        Src s;
+        s.init(B.bytes, v.p0, v.L);
+        gather_record<COMPAT>(B, sc, o, r, s);
+      }
+    }
+    wave_lds_sync();
   }
 }
 
@@ -821,16 +1005,18 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchem
     const uint32_t r = o.big_list[i];
     if (lane != 0 || o.status[r] != TFRG_OK) continue;
     const RecView v = rec_view(B, r);
-    gather_record<COMPAT>(B, sc, o, r, v);
+    Src s;
+    s.init(B.bytes, v.p0, v.L);
+    gather_record<COMPAT>(B, sc, o, r, s);
   }
 }
 
 // ------------------------------------------------------------------------------------------------
 // launcher
 // ------------------------------------------------------------------------------------------------
-constexpr int kLaneRep = 8;  // CRC table bank replication in the lane kernel
+constexpr int kLaneRep = 4;  // CRC table bank replication in the lane kernel
 
-constexpr size_t kLdsBudget = 96 * 1024;  // above this the dict state goes to the global column
+constexpr size_t kLdsBudget = 128 * 1024;  // above this the dict state goes to the global column
 
 const char* const kStageNames[kNumStages] = {"k_lane_count", "k_wave_count", "k_scan",
                                              "k_base",       "k_lane_gather", "k_wave_gather"};
@@ -842,15 +1028,16 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     if (ev) (void)hipEventRecord(ev[i], st);
   };
   const size_t tab_lds = 1024ull * kLaneRep * 4;
-  const size_t lane_lds = tab_lds + (size_t)sc.n_slots * kLaneBlock * 2;
+  const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
+  const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds;
   const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
   mark(kStageLaneCount);
   if (lane_lds <= kLdsBudget) {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
                        b, sc, o, d_tab, cfg.lane_max);
   } else {
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), tab_lds, st, b,
-                       sc, o, d_tab, cfg.lane_max);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock),
+                       tab_lds + stage_lds, st, b, sc, o, d_tab, cfg.lane_max);
   }
   mark(kStageWaveCount);
   if (wave_lds <= kLdsBudget) {
@@ -871,7 +1058,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                      sc.n_slots);
   mark(kStageLaneGather);
   if (sc.n_slots > 0) {
-    hipLaunchKernelGGL((k_lane_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), 0, st, b, sc, o,
+    hipLaunchKernelGGL((k_lane_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
                        cfg.lane_max);
   }
   mark(kStageWaveGather);

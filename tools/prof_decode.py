@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Profiling driver: a few device-resident decodes of one workload (for rocprofv3 runs).
+
+usage: prof_decode.py [--config c1|c2|c3] [--files N] [--iters K]
+"""
+import argparse
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+sys.path[:0] = [str(REPO / "tfrecords-reader_amd"), str(REPO)]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tfr_reader import hip, synth  # noqa: E402
+
+
+def workload(cfg: str, files: int):
+    if cfg == "c1":
+        pl = synth.c1_payloads(65536)
+    elif cfg == "c2":
+        pl = synth.c2_payloads(8189)
+    else:
+        pl = synth.c3_payloads(8192)
+    buf, st, en = synth.framed(pl)
+    return (buf, st, en), synth.replicate(buf, st, en, files)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c1")
+    ap.add_argument("--files", type=int, default=256)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--lane-max", type=int, default=None)
+    a = ap.parse_args()
+    sample, (big, st, en) = workload(a.config, a.files)
+    dev = torch.device("cuda", 0)
+    d_b = torch.zeros(big.size + 32, dtype=torch.uint8, device=dev)
+    d_b[: big.size].copy_(torch.from_numpy(big))
+    d_s = torch.from_numpy(st.view(np.int64)).to(dev)
+    d_e = torch.from_numpy(en.view(np.int64)).to(dev)
+    dec = hip.HipDecoder(0)
+    if a.lane_max is not None:
+        dec.set_lane_max(a.lane_max)
+    dec.decode(*sample)
+    s = torch.cuda.current_stream(dev)
+    dec.set_profiling(True)
+    for _ in range(a.iters):
+        dec.decode_device(d_b.data_ptr(), big.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0], stream=s.cuda_stream)
+        print({k: round(v, 4) for k, v in dec.profile_last().items()}, flush=True)
+    info = dec.info()
+    print("errors", info.n_errors, "miss", info.n_miss_records, "big", info.n_big, "bytes", big.size, "records", st.shape[0])
+
+
+if __name__ == "__main__":
+    main()
