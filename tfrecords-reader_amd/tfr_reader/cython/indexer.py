@@ -146,7 +146,10 @@ class TFRecordFileReader:
 
     def close(self) -> None:
         if self._map is not None:
-            self._map.close()
+            try:
+                self._map.close()
+            except BufferError:  # views handed out via .buffer are still alive: GC unmaps later
+                pass
             self._map = None
         if self._fd is not None:
             os.close(self._fd)

@@ -13,6 +13,8 @@ from collections import defaultdict
 from pathlib import Path
 from typing import Any
 
+import numpy as np
+
 from tfr_reader import _frame as F
 from tfr_reader import example, hip
 from tfr_reader.cython import indexer as native
@@ -71,8 +73,8 @@ def create_index_for_tfrecord(tfrecord_path: str, index_fn: example.IndexFunc | 
         size = os.path.getsize(tfrecord_path)
         ok = ptrs[:, 1] <= size
         res = None
-        if ok.any():
-            res = hip.default_decoder().decode(reader.buffer, ptrs[:, 0], ptrs[:, 1])
+        if ok.any():  # decode from a private copy: decoded values may outlive the reader
+            res = hip.default_decoder().decode(np.fromfile(tfrecord_path, dtype=np.uint8), ptrs[:, 0], ptrs[:, 1])
         for i in range(n):
             if not ok[i]:  # indexer.pyx:161-163
                 raise OSError("Failed to read record data")
