@@ -66,7 +66,7 @@ struct tfrg_ctx {
   // constants
   DBuf crc_tab, consts;
   // schema
-  DBuf ht, key_hash, key_off, key_blob, key_slot, slot_kind;
+  DBuf ht, key_hash, key_off, key_blob, key_slot, slot_kind, key_w;
   uint32_t n_keys = 0, n_slots = 0, ht_mask = 0;
   // host staging for tfrg_decode_host
   DBuf in_bytes, in_start, in_end;
@@ -131,7 +131,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
-                 &c->slot_kind, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
+                 &c->slot_kind, &c->key_w, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->granules, &c->ticket};
   for (DBuf* b : all) b->release();
@@ -167,10 +167,13 @@ int tfrg_profile_last(tfrg_ctx* c, float* ms, const char** names, int cap) {
   return k;
 }
 
-static uint32_t fnv1a(const uint8_t* p, uint64_t n) {
-  uint32_t h = 2166136261u;
-  for (uint64_t i = 0; i < n; ++i) h = (h ^ p[i]) * 16777619u;
-  return h;
+static void key_words(const uint8_t* p, uint64_t n, uint32_t* w0, uint32_t* w1) {
+  uint32_t a = 0, b = 0;
+  for (uint64_t i = 0; i < (n < 4 ? n : 4); ++i) a |= (uint32_t)p[i] << (8 * i);
+  if (n > 4)
+    for (uint64_t i = 0; i < 4; ++i) b |= (uint32_t)p[n - 4 + i] << (8 * i);
+  *w0 = a;
+  *w1 = b;
 }
 
 int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
@@ -180,7 +183,7 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   uint32_t hsz = 16;
   while (hsz < 2 * n_keys + 2) hsz <<= 1;
-  std::vector<uint32_t> ht(hsz, 0), hash(n_keys ? n_keys : 1), off(n_keys + 1);
+  std::vector<uint32_t> ht(hsz, 0), hash(n_keys ? n_keys : 1), off(n_keys + 1), kw(2ull * (n_keys ? n_keys : 1));
   std::vector<int32_t> ks(4ull * (n_keys ? n_keys : 1), -1);
   const uint64_t blob_len = n_keys ? key_offsets[n_keys] : 0;
   for (uint32_t k = 0; k < n_keys; ++k) {
@@ -189,7 +192,9 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
       return TFRG_E_ARG;
     }
     off[k] = (uint32_t)key_offsets[k];
-    hash[k] = fnv1a(key_blob + key_offsets[k], key_offsets[k + 1] - key_offsets[k]);
+    const uint64_t kl = key_offsets[k + 1] - key_offsets[k];
+    key_words(key_blob + key_offsets[k], kl, &kw[2ull * k], &kw[2ull * k + 1]);
+    hash[k] = key_hash_words((uint32_t)kl, kw[2ull * k], kw[2ull * k + 1]);
     ks[4ull * k] = (int32_t)(key_flags ? (key_flags[k] & 1u) : 0u);
     uint32_t j = hash[k] & (hsz - 1);
     while (ht[j]) j = (j + 1) & (hsz - 1);
@@ -204,7 +209,8 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
     ks[4ull * slot_key[s] + slot_kind[s]] = (int32_t)s;
   }
   if (c->ht.ensure(hsz * 4) || c->key_hash.ensure(hash.size() * 4) || c->key_off.ensure(off.size() * 4) ||
-      c->key_blob.ensure(blob_len + 16) || c->key_slot.ensure(ks.size() * 4) || c->slot_kind.ensure(n_slots + 16)) {
+      c->key_blob.ensure(blob_len + 16) || c->key_slot.ensure(ks.size() * 4) || c->slot_kind.ensure(n_slots + 16) ||
+      c->key_w.ensure(kw.size() * 4)) {
     set_error("schema allocation failed");
     return TFRG_E_NOMEM;
   }
@@ -213,6 +219,7 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   HIP_TRY(hipMemcpy(c->key_off.p, off.data(), off.size() * 4, hipMemcpyHostToDevice));
   if (blob_len) HIP_TRY(hipMemcpy(c->key_blob.p, key_blob, blob_len, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->key_slot.p, ks.data(), ks.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->key_w.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice));
   if (n_slots) HIP_TRY(hipMemcpy(c->slot_kind.p, slot_kind, n_slots, hipMemcpyHostToDevice));
   c->n_keys = n_keys;
   c->n_slots = n_slots;
@@ -231,6 +238,7 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.key_blob = c->key_blob.as<uint8_t>();
   s.key_slot = c->key_slot.as<int32_t>();
   s.slot_kind = c->slot_kind.as<uint8_t>();
+  s.key_w = c->key_w.as<uint32_t>();
   return s;
 }
 

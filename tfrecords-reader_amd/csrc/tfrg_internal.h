@@ -18,7 +18,19 @@ struct DevSchema {
   const uint8_t* key_blob;
   const int32_t* key_slot;     // [n_keys*4]: [0] flags (bit0 invalid UTF-8), [1..3] slot per kind or -1
   const uint8_t* slot_kind;    // [n_slots]
+  const uint32_t* key_w;       // [n_keys][2]: first / last 4 key bytes (see key_hash_words)
 };
+
+// Key hash over (length, first 4 bytes, last 4 bytes), all little-endian and zero padded:
+// w0 = bytes [0, min(n,4)), w1 = n > 4 ? bytes [n-4, n) : 0. For n <= 8 the triple (n, w0, w1)
+// IS the key, so a table hit needs no byte compare.
+__host__ __device__ inline uint32_t key_hash_words(uint32_t n, uint32_t w0, uint32_t w1) {
+  uint32_t h = n * 0x9E3779B1u;
+  h ^= w0 * 0x85EBCA77u;
+  h = (h << 13) | (h >> 19);
+  h ^= w1 * 0xC2B2AE3Du;
+  return h ^ (h >> 16);
+}
 
 struct DevBatch {
   const uint8_t* bytes;        // records (framed or bare payloads); readable to round_up(nbytes,16)

@@ -340,19 +340,23 @@ struct CountSink {
   // key bytes -> key id; -1 unknown, -2 interned as invalid UTF-8
   template <class S>
   __device__ int lookup(S& s, int64_t off, int64_t len) {
-    uint32_t h = 2166136261u;
-    for (int64_t i = 0; i < len; ++i) h = (h ^ s.at(off + i)) * 16777619u;
-    if (sc->n_keys == 0) return -1;
+    if (sc->n_keys == 0 || len > 0xffffffffll) return -1;
+    uint32_t w0 = 0, w1 = 0;
+    for (int64_t i = 0; i < (len < 4 ? len : 4); ++i) w0 |= s.at(off + i) << (8 * i);
+    if (len > 4)
+      for (int64_t i = 0; i < 4; ++i) w1 |= s.at(off + len - 4 + i) << (8 * i);
+    const uint32_t h = key_hash_words((uint32_t)len, w0, w1);
     uint32_t j = h & sc->ht_mask;
     for (uint32_t probe = 0; probe <= sc->ht_mask; ++probe) {
       const uint32_t e = sc->ht[j];
       if (!e) return -1;
       const uint32_t kid = e - 1;
       const uint32_t ko = sc->key_off[kid];
-      if (sc->key_hash[kid] == h && (int64_t)(sc->key_off[kid + 1] - ko) == len) {
+      if (sc->key_hash[kid] == h && (int64_t)(sc->key_off[kid + 1] - ko) == len &&
+          sc->key_w[2 * kid] == w0 && sc->key_w[2 * kid + 1] == w1) {
         const uint8_t* kb = sc->key_blob + ko;
         bool eq = true;
-        for (int64_t i = 0; i < len && eq; ++i) eq = s.at(off + i) == kb[i];
+        for (int64_t i = 4; i < len - 4 && eq; ++i) eq = s.at(off + i) == kb[i];
         if (eq) return (sc->key_slot[kid * 4] & 1) ? -2 : (int)kid;
       }
       j = (j + 1) & sc->ht_mask;
@@ -645,6 +649,167 @@ __device__ uint32_t crc_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsT
   return ~c;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Fast walker for canonical, valid records in the LDS stage. Single pass, 32-bit positions,
+// 4-byte varint reads, word-wise key match, terminator popcount for packed int64. It accepts only
+// records whose reference result is unambiguous (every field where a serializer puts it, no
+// error, no duplicate or unknown key, tag/length varints <= 4 bytes, no varint overrun) and
+// returns kBail for anything else; the lane then re-walks that record with the exact walker.
+// ------------------------------------------------------------------------------------------------
+constexpr int kBail = -1;
+
+struct FastSrc {
+  const uint8_t* l;  // stage
+  uint32_t p;        // payload offset in the stage
+  uint32_t L;        // payload length
+  // 4 payload bytes at i (i <= L); bytes at index >= L read as 0 (the NUL terminator and beyond)
+  __device__ __forceinline__ uint32_t w4(uint32_t i) const {
+    uint32_t w = lds_u32u(l, p + i);
+    const uint32_t rem = L - i;
+    if (rem < 4) w &= (1u << (8 * rem)) - 1u;
+    return w;
+  }
+};
+
+// varint of <= 4 bytes (values < 2^28: identical in compat and spec mode); false = bail
+__device__ __forceinline__ bool fv32(const FastSrc& s, uint32_t& pos, uint32_t& v) {
+  if (pos > s.L) return false;
+  const uint32_t w = s.w4(pos);
+  const uint32_t term = ~w & 0x80808080u;
+  if (!term) return false;
+  const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
+  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+  v = x & ((1u << (7u * nb)) - 1u);
+  pos += nb;
+  return true;
+}
+
+// a length-delimited field inside [pos, end): returns its field number, payload offset and length
+__device__ __forceinline__ bool ffield(const FastSrc& s, uint32_t& pos, uint32_t end, uint32_t& fn, uint32_t& off,
+                                       uint32_t& len) {
+  uint32_t key;
+  if (!fv32(s, pos, key) || (key & 7u) != 2u) return false;
+  fn = key >> 3;
+  if (!fv32(s, pos, len) || pos > end || len > end - pos) return false;
+  off = pos;
+  pos += len;
+  return true;
+}
+
+// number of varints in a packed chunk [o, e) that ends on a terminator, with no varint longer
+// than 10 bytes (else bail: 'Too many bytes' / overrun semantics are the exact walker's)
+__device__ __forceinline__ bool count_packed(const FastSrc& s, uint32_t o, uint32_t e, uint32_t& cnt) {
+  uint32_t run = 0, terms = 0, last = 0x80u;
+  for (uint32_t i = o; i < e; i += 4) {
+    const uint32_t w = lds_u32u(s.l, s.p + i);
+    const uint32_t rem = e - i;
+    const uint32_t valid = rem >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * rem)) - 1u));
+    const uint32_t term = ~w & valid;
+    const uint32_t nvalid = __popc(valid);
+    if (!term) {
+      run += nvalid;
+      if (run >= 10) return false;
+    } else {
+      if (run + (__builtin_ctz(term) >> 3) >= 10) return false;
+      run = nvalid - 1u - ((31u - __builtin_clz(term)) >> 3);
+      terms += __popc(term);
+    }
+    last = (w >> (8 * (nvalid - 1u))) & 0x80u;
+  }
+  if (e > o && last) return false;  // the last varint runs past the chunk
+  cnt = terms;
+  return true;
+}
+
+__device__ __forceinline__ bool fast_list_count(const FastSrc& s, uint32_t kind, uint32_t lo, uint32_t ll,
+                                                uint32_t& cnt) {
+  uint32_t q = lo, c = 0;
+  const uint32_t le = lo + ll;
+  while (q < le) {
+    uint32_t fn, co, cl;
+    if (!ffield(s, q, le, fn, co, cl) || fn != 1u) return false;
+    if (kind == TFRG_KIND_BYTES) {
+      ++c;
+    } else if (kind == TFRG_KIND_FLOAT) {
+      if (cl & 3u) return false;
+      c += cl >> 2;
+    } else {
+      uint32_t k;
+      if (!count_packed(s, co, co + cl, k)) return false;
+      c += k;
+    }
+  }
+  cnt = c;
+  return true;
+}
+
+// key id for key bytes at [ko, ko+kl) of the payload; -1 = not a plain hit (bail)
+__device__ __forceinline__ int fast_lookup(const FastSrc& s, const DevSchema& sc, uint32_t ko, uint32_t kl) {
+  if (kl > 8u || sc.n_keys == 0) return -1;  // longer keys: exact walker (byte compare)
+  uint32_t w0 = lds_u32u(s.l, s.p + ko);
+  if (kl < 4) w0 &= (1u << (8 * kl)) - 1u;
+  const uint32_t w1 = kl > 4 ? lds_u32u(s.l, s.p + ko + kl - 4) : 0u;
+  const uint32_t h = key_hash_words(kl, w0, w1);
+  uint32_t j = h & sc.ht_mask;
+  for (uint32_t probe = 0; probe <= sc.ht_mask; ++probe) {
+    const uint32_t e = sc.ht[j];
+    if (!e) return -1;
+    const uint32_t kid = e - 1;
+    if (sc.key_hash[kid] == h && sc.key_off[kid + 1] - sc.key_off[kid] == kl && sc.key_w[2 * kid] == w0 &&
+        sc.key_w[2 * kid + 1] == w1)
+      return (sc.key_slot[kid * 4] & 1) ? -1 : (int)kid;
+    j = (j + 1) & sc.ht_mask;
+  }
+  return -1;
+}
+
+// Returns TFRG_OK with the dict in sink.ord / count / loc, or kBail.
+__device__ int fast_walk(const FastSrc& s, const DevSchema& sc, CountSink& sink) {
+  uint32_t pos = 0;
+  const uint32_t L = s.L;
+  bool have = false;
+  uint64_t seen = 0;  // key ids < 64 already in the dict (a duplicate key bails)
+  while (pos < L) {
+    uint32_t fn, fo, fl;
+    if (have || !ffield(s, pos, L, fn, fo, fl) || fn != 1u) return kBail;
+    have = true;
+    uint32_t q = fo;
+    const uint32_t fe = fo + fl;
+    while (q < fe) {
+      uint32_t en, eo, el;
+      if (!ffield(s, q, fe, en, eo, el) || en != 1u) return kBail;
+      uint32_t e = eo;
+      const uint32_t ee = eo + el;
+      uint32_t kn, ko, kl, vn, vo, vl;
+      if (!ffield(s, e, ee, kn, ko, kl) || kn != 1u) return kBail;
+      if (!ffield(s, e, ee, vn, vo, vl) || vn != 2u || e != ee) return kBail;
+      const int kid = fast_lookup(s, sc, ko, kl);
+      if (kid < 0) return kBail;
+      uint32_t g = vo, kind, lo, ll, cnt;
+      if (!ffield(s, g, vo + vl, kind, lo, ll) || g != vo + vl || kind < 1u || kind > 3u) return kBail;
+      if (!fast_list_count(s, kind, lo, ll, cnt)) return kBail;
+      const int slot = sc.key_slot[kid * 4 + (int)kind];
+      if (slot < 0) return kBail;
+      if (kid < 64) {
+        const uint64_t bit = 1ull << kid;
+        if (seen & bit) return kBail;
+        seen |= bit;
+      } else {
+        for (int k = 1; k <= 3; ++k) {
+          const int s2 = sc.key_slot[kid * 4 + k];
+          if (s2 >= 0 && sink.ord[(size_t)s2 * sink.ostride]) return kBail;
+        }
+      }
+      if (sink.rank >= 65534u) return kBail;
+      sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(++sink.rank);
+      const size_t at = (size_t)slot * sink.n + sink.r;
+      sink.o->count[at] = cnt;
+      sink.o->loc[at] = make_uint2(lo, ll);
+    }
+  }
+  return have ? TFRG_OK : kBail;
+}
+
 // Framing verdicts + reference walk of one record (lane-per-record), from the stage or from HBM.
 template <int R, bool COMPAT, bool STAGED>
 __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc, uint32_t r, RecView& v,
@@ -690,9 +855,15 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
   for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
   int status;
   if constexpr (STAGED) {
-    LdsSrc s;
-    s.init(stage, lo16, v.p0, v.L);
-    status = walk_example<COMPAT>(s, sink, aux);
+    const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L};
+    status = fast_walk(fs, sc, sink);
+    if (status == kBail) {  // non-canonical record: exact reference walk from the same stage
+      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+      sink.rank = 0;
+      LdsSrc s;
+      s.init(stage, lo16, v.p0, v.L);
+      status = walk_example<COMPAT>(s, sink, aux);
+    }
   } else {
     Src s;
     s.init(B.bytes, v.p0, v.L);
