@@ -66,7 +66,7 @@ struct tfrg_ctx {
   // constants
   DBuf crc_tab, consts;
   // schema
-  DBuf ht, key_hash, key_off, key_blob, key_slot, slot_kind, key_w;
+  DBuf ht, key_hash, key_off, key_blob, key_slot, slot_kind, key_w, krec;
   uint32_t n_keys = 0, n_slots = 0, ht_mask = 0;
   // host staging for tfrg_decode_host
   DBuf in_bytes, in_start, in_end;
@@ -131,7 +131,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
-                 &c->slot_kind, &c->key_w, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
+                 &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->granules, &c->ticket};
   for (DBuf* b : all) b->release();
@@ -220,6 +220,21 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   if (blob_len) HIP_TRY(hipMemcpy(c->key_blob.p, key_blob, blob_len, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->key_slot.p, ks.data(), ks.size() * 4, hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(c->key_w.p, kw.data(), kw.size() * 4, hipMemcpyHostToDevice));
+  std::vector<uint32_t> kr((size_t)kKrWords * (n_keys ? n_keys : 1), 0);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    uint32_t* r = &kr[(size_t)kKrWords * k];
+    r[kKrHash] = hash[k];
+    r[kKrLen] = (uint32_t)(key_offsets[k + 1] - key_offsets[k]);
+    r[kKrW0] = kw[2ull * k];
+    r[kKrW1] = kw[2ull * k + 1];
+    for (int kind = 1; kind <= 3; ++kind) r[kKrSlot1 + kind - 1] = (uint32_t)ks[4ull * k + kind];
+    r[kKrFlags] = (uint32_t)ks[4ull * k];
+  }
+  if (c->krec.ensure(kr.size() * 4)) {
+    set_error("schema allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(c->krec.p, kr.data(), kr.size() * 4, hipMemcpyHostToDevice));
   if (n_slots) HIP_TRY(hipMemcpy(c->slot_kind.p, slot_kind, n_slots, hipMemcpyHostToDevice));
   c->n_keys = n_keys;
   c->n_slots = n_slots;
@@ -239,6 +254,7 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.key_slot = c->key_slot.as<int32_t>();
   s.slot_kind = c->slot_kind.as<uint8_t>();
   s.key_w = c->key_w.as<uint32_t>();
+  s.krec = c->krec.as<uint32_t>();
   return s;
 }
 

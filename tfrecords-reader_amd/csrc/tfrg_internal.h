@@ -19,7 +19,13 @@ struct DevSchema {
   const int32_t* key_slot;     // [n_keys*4]: [0] flags (bit0 invalid UTF-8), [1..3] slot per kind or -1
   const uint8_t* slot_kind;    // [n_slots]
   const uint32_t* key_w;       // [n_keys][2]: first / last 4 key bytes (see key_hash_words)
+  const uint32_t* krec;        // [n_keys][8] packed key record, see KeyRec
 };
+
+// Packed per-key record (8 x u32) staged into LDS by the lane kernels' fast path.
+enum KeyRec : uint32_t { kKrHash = 0, kKrLen, kKrW0, kKrW1, kKrSlot1, kKrSlot2, kKrSlot3, kKrFlags, kKrWords };
+constexpr uint32_t kLdsMaxKeys = 256;     // key tables up to this size are staged into LDS
+constexpr uint32_t kLdsMaxHt = 1024;      // hash-table entries staged into LDS
 
 // Key hash over (length, first 4 bytes, last 4 bytes), all little-endian and zero padded:
 // w0 = bytes [0, min(n,4)), w1 = n > 4 ? bytes [n-4, n) : 0. For n <= 8 the triple (n, w0, w1)

@@ -743,28 +743,34 @@ __device__ __forceinline__ bool fast_list_count(const FastSrc& s, uint32_t kind,
   return true;
 }
 
+// LDS copy of the key table for the fast path: hash table + packed key records
+struct LdsKeys {
+  const uint32_t* ht;    // [mask+1] key id + 1
+  const uint32_t* rec;   // [n_keys][kKrWords]
+  uint32_t mask;
+};
+
 // key id for key bytes at [ko, ko+kl) of the payload; -1 = not a plain hit (bail)
-__device__ __forceinline__ int fast_lookup(const FastSrc& s, const DevSchema& sc, uint32_t ko, uint32_t kl) {
-  if (kl > 8u || sc.n_keys == 0) return -1;  // longer keys: exact walker (byte compare)
+__device__ __forceinline__ int fast_lookup(const FastSrc& s, const LdsKeys& K, uint32_t ko, uint32_t kl) {
+  if (kl > 8u) return -1;  // longer keys: exact walker (byte compare)
   uint32_t w0 = lds_u32u(s.l, s.p + ko);
   if (kl < 4) w0 &= (1u << (8 * kl)) - 1u;
   const uint32_t w1 = kl > 4 ? lds_u32u(s.l, s.p + ko + kl - 4) : 0u;
   const uint32_t h = key_hash_words(kl, w0, w1);
-  uint32_t j = h & sc.ht_mask;
-  for (uint32_t probe = 0; probe <= sc.ht_mask; ++probe) {
-    const uint32_t e = sc.ht[j];
+  uint32_t j = h & K.mask;
+  for (uint32_t probe = 0; probe <= K.mask; ++probe) {
+    const uint32_t e = K.ht[j];
     if (!e) return -1;
-    const uint32_t kid = e - 1;
-    if (sc.key_hash[kid] == h && sc.key_off[kid + 1] - sc.key_off[kid] == kl && sc.key_w[2 * kid] == w0 &&
-        sc.key_w[2 * kid + 1] == w1)
-      return (sc.key_slot[kid * 4] & 1) ? -1 : (int)kid;
-    j = (j + 1) & sc.ht_mask;
+    const uint32_t* r = K.rec + (e - 1) * kKrWords;
+    if (r[kKrHash] == h && r[kKrLen] == kl && r[kKrW0] == w0 && r[kKrW1] == w1)
+      return (r[kKrFlags] & 1u) ? -1 : (int)(e - 1);
+    j = (j + 1) & K.mask;
   }
   return -1;
 }
 
 // Returns TFRG_OK with the dict in sink.ord / count / loc, or kBail.
-__device__ int fast_walk(const FastSrc& s, const DevSchema& sc, CountSink& sink) {
+__device__ int fast_walk(const FastSrc& s, const LdsKeys& K, CountSink& sink) {
   uint32_t pos = 0;
   const uint32_t L = s.L;
   bool have = false;
@@ -783,20 +789,21 @@ __device__ int fast_walk(const FastSrc& s, const DevSchema& sc, CountSink& sink)
       uint32_t kn, ko, kl, vn, vo, vl;
       if (!ffield(s, e, ee, kn, ko, kl) || kn != 1u) return kBail;
       if (!ffield(s, e, ee, vn, vo, vl) || vn != 2u || e != ee) return kBail;
-      const int kid = fast_lookup(s, sc, ko, kl);
+      const int kid = fast_lookup(s, K, ko, kl);
       if (kid < 0) return kBail;
+      const uint32_t* kr = K.rec + (uint32_t)kid * kKrWords;
       uint32_t g = vo, kind, lo, ll, cnt;
       if (!ffield(s, g, vo + vl, kind, lo, ll) || g != vo + vl || kind < 1u || kind > 3u) return kBail;
       if (!fast_list_count(s, kind, lo, ll, cnt)) return kBail;
-      const int slot = sc.key_slot[kid * 4 + (int)kind];
+      const int slot = (int)kr[kKrSlot1 + kind - 1];
       if (slot < 0) return kBail;
       if (kid < 64) {
         const uint64_t bit = 1ull << kid;
         if (seen & bit) return kBail;
         seen |= bit;
       } else {
-        for (int k = 1; k <= 3; ++k) {
-          const int s2 = sc.key_slot[kid * 4 + k];
+        for (int k = 0; k < 3; ++k) {
+          const int s2 = (int)kr[kKrSlot1 + k];
           if (s2 >= 0 && sink.ord[(size_t)s2 * sink.ostride]) return kBail;
         }
       }
@@ -814,7 +821,7 @@ __device__ int fast_walk(const FastSrc& s, const DevSchema& sc, CountSink& sink)
 template <int R, bool COMPAT, bool STAGED>
 __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc, uint32_t r, RecView& v,
                                          CountSink& sink, const LdsTab<R>& T, const uint8_t* stage, uint64_t lo16,
-                                         int64_t& aux) {
+                                         const LdsKeys& K, bool fast_ok, int64_t& aux) {
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
   if (framed) {
@@ -856,7 +863,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
   int status;
   if constexpr (STAGED) {
     const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L};
-    status = fast_walk(fs, sc, sink);
+    status = fast_ok ? fast_walk(fs, K, sink) : kBail;
     if (status == kBail) {  // non-canonical record: exact reference walk from the same stage
       for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
       sink.rank = 0;
@@ -876,7 +883,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
 // GORD: keep the per-record dict state in the global `order` column instead of LDS (key tables too
 // large for LDS); same results, slower.
 template <int R, bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -884,9 +891,19 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 1024 * R);   // [n_slots][kLaneBlock]
   const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * kLaneBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
-  uint8_t* stage = reinterpret_cast<uint8_t*>(lds + 1024 * R) + ord_bytes + wib * kStageStride;
+  uint8_t* stage_all = reinterpret_cast<uint8_t*>(lds + 1024 * R) + ord_bytes;
+  uint8_t* stage = stage_all + wib * kStageStride;
+  // key table for the fast path (after the 4 wave stages)
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
+  uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
+  uint32_t* krec = kht + kLdsMaxHt;
   for (uint32_t i = threadIdx.x; i < 1024u * R; i += kLaneBlock) tab[i] = crc_tab[i / R];
+  if (fast_ok) {
+    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
+  }
   __syncthreads();
+  const LdsKeys K{kht, krec, sc.ht_mask};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
 
   for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
@@ -921,8 +938,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_count(DevBatch B, DevSchema
                      B.n, r, v.p0, false, true};
       int status = v.status;
       if (status == TFRG_OK) {
-        status = staged ? count_one<R, COMPAT, true>(B, sc, r, v, sink, T, stage, lo16, aux)
-                        : count_one<R, COMPAT, false>(B, sc, r, v, sink, T, stage, lo16, aux);
+        status = staged ? count_one<R, COMPAT, true>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux)
+                        : count_one<R, COMPAT, false>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux);
       }
       sink.finalize(status == TFRG_OK);
       record_result(o, r, status, aux, v.verdict);
@@ -1200,7 +1217,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   };
   const size_t tab_lds = 1024ull * kLaneRep * 4;
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
-  const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds;
+  const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
+                              ? (kLdsMaxHt + (size_t)sc.n_keys * kKrWords) * 4 : 0;
+  const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds + keys_lds;
   const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
   mark(kStageLaneCount);
   if (lane_lds <= kLdsBudget) {
@@ -1208,7 +1227,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        b, sc, o, d_tab, cfg.lane_max);
   } else {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock),
-                       tab_lds + stage_lds, st, b, sc, o, d_tab, cfg.lane_max);
+                       tab_lds + stage_lds + keys_lds, st, b, sc, o, d_tab, cfg.lane_max);
   }
   mark(kStageWaveCount);
   if (wave_lds <= kLdsBudget) {
