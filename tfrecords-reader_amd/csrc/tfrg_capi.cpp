@@ -72,7 +72,7 @@ struct tfrg_ctx {
   DBuf in_bytes, in_start, in_end;
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
-  DBuf i64, f32, b_off, b_len, big_list, miss, info, granules, ticket;
+  DBuf i64, f32, b_off, b_len, big_list, miss, info, tsum;
   // last batch
   uint32_t n = 0;
   uint64_t nbytes = 0;
@@ -133,7 +133,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
-                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->granules, &c->ticket};
+                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->tsum};
   for (DBuf* b : all) b->release();
   if (c->have_events)
     for (auto& e : c->ev) (void)hipEventDestroy(e);
@@ -281,22 +281,20 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
               c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
-              c->granules.cap < (uint64_t)S * n_tiles * 8 + 8;
+              c->tsum.cap < (uint64_t)S * n_tiles * 4 + 8;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
       c->count.ensure(S * nn * 4) || c->loc.ensure(S * nn * 8) || c->rs.ensure(S * (nn + 1) * 4) ||
       c->slot_base.ensure((S + 1) * 8) || c->totals.ensure((S + 1) * 4) || c->kind_totals.ensure(32) ||
       c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
       c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->miss.ensure(kMissCap * 16ull) ||
-      c->info.ensure(kInfoCount * 4) || c->granules.ensure((uint64_t)S * n_tiles * 8 + 8) || c->ticket.ensure(16)) {
+      c->info.ensure(kInfoCount * 4) || c->tsum.ensure((uint64_t)S * n_tiles * 4 + 8)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
   // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
   HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
   HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
-  HIP_TRY(hipMemsetAsync(c->ticket.p, 0, 16, st));
-  if (S && n_tiles) HIP_TRY(hipMemsetAsync(c->granules.p, 0, (size_t)S * n_tiles * 8, st));
   if (S) HIP_TRY(hipMemsetAsync(c->totals.p, 0, S * 4, st));
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
 
@@ -329,8 +327,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.miss = c->miss.as<uint32_t>();
   o.miss_cap = kMissCap;
   o.info = c->info.as<uint32_t>();
-  o.granules = c->granules.as<uint64_t>();
-  o.ticket = c->ticket.as<uint32_t>();
+  o.tsum = c->tsum.as<uint32_t>();
   LaunchCfg cfg;
   const uint64_t lane_blocks = (n + 255) / 256;
   const uint64_t lane_cap = (uint64_t)c->num_cus * 8;

@@ -54,7 +54,7 @@ enum InfoIdx : uint32_t {
   kInfoMissRecords = 2,  // records with a schema miss
   kInfoMissEntries = 3,  // miss entries appended (may exceed capacity)
   kInfoBig = 4,          // records routed to the wave-per-record kernels
-  kInfoScanTimeout = 5,  // look-back spin gave up (must stay 0)
+  kInfoScanTimeout = 5,  // reserved (always 0: the scan has no inter-workgroup waits)
   kInfoCount = 16
 };
 
@@ -78,8 +78,7 @@ struct DevOut {
   uint32_t* miss;        // [miss_cap][4] (record, kind, key abs offset, key length)
   uint32_t miss_cap;
   uint32_t* info;        // [kInfoCount]
-  uint64_t* granules;    // [n_slots][n_tiles] scan look-back state
-  uint32_t* ticket;      // scan tile ticket
+  uint32_t* tsum;        // [n_slots][n_tiles] scan tile sums / prefixes
 };
 
 // flags (mirrors include/tfrg.h)
@@ -88,7 +87,7 @@ constexpr uint32_t kFlagSpecVarint = 2u;
 constexpr uint32_t kFlagNoCrc = 4u;
 
 constexpr int kScanBlock = 256;
-constexpr int kScanItems = 8;
+constexpr int kScanItems = 16;
 constexpr uint32_t kScanTile = kScanBlock * kScanItems;
 
 // launchers (tfrg_kernels.hip)

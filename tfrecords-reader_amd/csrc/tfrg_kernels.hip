@@ -11,8 +11,8 @@
 //   2. k_wave_count  : one WAVEFRONT per large record: the CRC is split over 64 lanes in 16-byte
 //                      chunks (coalesced 1 KiB rounds) and recombined with GF(2) shift operators;
 //                      the structure walk runs wave-uniform.
-//   3. k_scan        : per-slot exclusive scan of the counts (single pass, decoupled look-back
-//                      over 8-byte {status,value} granules, agent-scope relaxed atomics).
+//   3. k_scan_*      : per-slot exclusive scan of the counts (reduce -> spine -> downsweep;
+//                      no inter-workgroup waiting).
 //   4. k_base        : per-kind column bases.
 //   5. k_lane_gather / k_wave_gather : write the int64 / float / bytes-view values of every
 //                      present slot into per-slot contiguous columns.
@@ -662,6 +662,7 @@ struct FastSrc {
   const uint8_t* l;  // stage
   uint32_t p;        // payload offset in the stage
   uint32_t L;        // payload length
+  uint64_t base;     // absolute offset of the payload in the input (bytes views)
   // 4 payload bytes at i (i <= L); bytes at index >= L read as 0 (the NUL terminator and beyond)
   __device__ __forceinline__ uint32_t w4(uint32_t i) const {
     uint32_t w = lds_u32u(l, p + i);
@@ -862,7 +863,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
   for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
   int status;
   if constexpr (STAGED) {
-    const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L};
+    const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
     status = fast_ok ? fast_walk(fs, K, sink) : kBail;
     if (status == kBail) {  // non-canonical record: exact reference walk from the same stage
       for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
@@ -1001,89 +1002,102 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
 }
 
 // ------------------------------------------------------------------------------------------------
-// Per-slot exclusive scan, single pass with decoupled look-back.
-// Granule = {status:32 | value:32}; status 1 = tile aggregate, 2 = inclusive prefix. Written and
-// read with relaxed agent-scope 8-byte atomics: the data is the flag (Guideline 16 R2). Tiles are
-// taken in ticket order, so every tile a block waits on is already resident.
+// Per-slot exclusive scan of the counts: reduce -> spine -> downsweep. Fully parallel (no
+// inter-workgroup waiting); counts are read twice, row splits written once.
+// Tile = kScanBlock threads x kScanItems consecutive u32 per thread (16-byte loads).
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kScanBlock) void k_scan(const uint32_t* __restrict__ count, uint32_t* rs,
-                                                     uint32_t* totals, uint64_t* gran, uint32_t* ticket,
-                                                     uint32_t* info, uint32_t n, uint32_t n_tiles) {
-  __shared__ uint32_t s_t, s_prefix;
-  __shared__ uint32_t s_wsum[kScanBlock / 64];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u, wid = tid >> 6;
-  if (tid == 0) s_t = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t t = s_t;
-  const uint32_t slot = t / n_tiles, tile = t % n_tiles;
-  const uint32_t* c = count + (size_t)slot * n;
-  uint32_t* out = rs + (size_t)slot * (n + 1);
-  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)tid * kScanItems;
-  uint32_t v[kScanItems];
-  uint32_t sum = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    const uint64_t idx = base + i;
-    v[i] = idx < n ? c[idx] : 0u;
-    sum += v[i];
-  }
-  // block exclusive scan of the per-thread sums
-  uint32_t incl = sum;
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  uint32_t incl = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
     const uint32_t y = __shfl_up(incl, d, 64);
     if (lane >= (uint32_t)d) incl += y;
   }
-  if (lane == 63) s_wsum[wid] = incl;
+  if (lane == 63) s_w[wid] = incl;
   __syncthreads();
-  uint32_t wpre = 0, agg = 0;
+  uint32_t pre = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < kScanBlock / 64; ++w) {
-    if ((uint32_t)w < wid) wpre += s_wsum[w];
-    agg += s_wsum[w];
-  }
-  const uint32_t excl = wpre + incl - sum;
-  if (tid == 0) {
-    uint64_t* g = gran + (size_t)slot * n_tiles;
-    uint32_t prefix = 0;
-    if (tile == 0) {
-      __hip_atomic_store(&g[0], (2ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&g[tile], (1ull << 32) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      int64_t j = (int64_t)tile - 1;
-      uint32_t spins = 0;
-      while (j >= 0) {
-        const uint64_t x = __hip_atomic_load(&g[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t stt = (uint32_t)(x >> 32);
-        if (stt == 0) {
-          if (++spins > (1u << 22)) {  // never hang the GPU: give up and flag
-            atomicAdd(&info[kInfoScanTimeout], 1u);
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-          continue;
-        }
-        prefix += (uint32_t)x;
-        if (stt == 2) break;
-        --j;
-      }
-      __hip_atomic_store(&g[tile], (2ull << 32) | (uint64_t)(prefix + agg), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_prefix = prefix;
+    const uint32_t x = s_w[w];
+    pre += (uint32_t)w < wid ? x : 0u;
+    tot += x;
   }
   __syncthreads();
-  uint32_t run = s_prefix + excl;
+  total = tot;
+  return pre + incl - v;
+}
+
+__device__ __forceinline__ void load_items(const uint32_t* c, uint64_t base, uint32_t n, uint32_t (&v)[kScanItems]) {
+  if (base + kScanItems <= n && ((base & 3u) == 0)) {
+#pragma unroll
+    for (int i = 0; i < kScanItems; i += 4) {
+      const uint4 q = *reinterpret_cast<const uint4*>(c + base + i);
+      v[i] = q.x;
+      v[i + 1] = q.y;
+      v[i + 2] = q.z;
+      v[i + 3] = q.w;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i) v[i] = base + i < n ? c[base + i] : 0u;
+  }
+}
+
+// phase 1: per-tile sums -> tsum[slot][tile]
+__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint32_t* __restrict__ count, uint32_t* tsum,
+                                                            uint32_t n, uint32_t n_tiles) {
+  __shared__ uint32_t s_w[kScanBlock / 64];
+  const uint32_t slot = blockIdx.y, tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  load_items(count + (size_t)slot * n, base, n, v);
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) sum += v[i];
+  uint32_t total;
+  block_excl_scan(sum, s_w, total);
+  if (threadIdx.x == 0) tsum[(size_t)slot * n_tiles + tile] = total;
+}
+
+// phase 2: exclusive scan of the tile sums of one slot (one workgroup per slot)
+__global__ __launch_bounds__(kScanBlock) void k_scan_spine(uint32_t* tsum, uint32_t* totals, uint32_t n_tiles) {
+  __shared__ uint32_t s_w[kScanBlock / 64];
+  uint32_t* t = tsum + (size_t)blockIdx.x * n_tiles;
+  uint32_t carry = 0;
+  for (uint32_t b = 0; b < n_tiles; b += kScanBlock) {
+    const uint32_t i = b + threadIdx.x;
+    const uint32_t v = i < n_tiles ? t[i] : 0u;
+    uint32_t total;
+    const uint32_t ex = block_excl_scan(v, s_w, total);
+    if (i < n_tiles) t[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
+}
+
+// phase 3: row splits = tile prefix + in-tile exclusive scan
+__global__ __launch_bounds__(kScanBlock) void k_scan_down(const uint32_t* __restrict__ count, uint32_t* rs,
+                                                          const uint32_t* __restrict__ tsum,
+                                                          const uint32_t* __restrict__ totals, uint32_t n,
+                                                          uint32_t n_tiles) {
+  __shared__ uint32_t s_w[kScanBlock / 64];
+  const uint32_t slot = blockIdx.y, tile = blockIdx.x;
+  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
+  uint32_t v[kScanItems];
+  load_items(count + (size_t)slot * n, base, n, v);
+  uint32_t sum = 0;
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) sum += v[i];
+  uint32_t total;
+  uint32_t run = tsum[(size_t)slot * n_tiles + tile] + block_excl_scan(sum, s_w, total);
+  uint32_t* out = rs + (size_t)slot * (n + 1);
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    const uint64_t idx = base + i;
-    if (idx < n) out[idx] = run;
+    if (base + i < n) out[base + i] = run;
     run += v[i];
   }
-  if (tile == n_tiles - 1 && tid == kScanBlock - 1) {
-    out[n] = run;
-    totals[slot] = run;
-  }
+  if (tile == 0 && threadIdx.x == 0) out[n] = totals[slot];
 }
 
 __global__ void k_base(const uint32_t* totals, const uint8_t* slot_kind, uint64_t* slot_base,
@@ -1134,6 +1148,73 @@ __device__ void list_gather(S& s, const DevOut& o, int kind, int64_t lo, int64_t
   }
 }
 
+// one int64 varint at `pos` of a validated packed chunk ending at `e` (fast path): <= 4 bytes from
+// one word, longer ones byte by byte with the reference's compat semantics; false = bail
+template <bool COMPAT>
+__device__ __forceinline__ bool fast_value(const FastSrc& s, uint32_t& pos, uint32_t e, int64_t& val) {
+  const uint32_t w = s.w4(pos);
+  const uint32_t term = ~w & 0x80808080u;
+  if (term) {
+    const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
+    if (pos + nb > e) return false;
+    const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+    val = (int64_t)(x & ((1u << (7u * nb)) - 1u));
+    pos += nb;
+    return true;
+  }
+  uint64_t spec = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+  uint32_t lo32 = (uint32_t)spec;
+  bool neg = false;
+  uint32_t k = 4;
+  for (;; ++k) {
+    if (k >= 10 || pos + k >= e) return false;  // too long or runs past the chunk: exact path
+    const uint32_t b = s.l[s.p + pos + k];
+    const uint32_t g = b & 0x7fu;
+    spec |= k < 10 ? ((uint64_t)g << (7 * k)) : 0;
+    const uint32_t t = g << ((7 * k) & 31);
+    lo32 |= t;
+    neg |= (t >> 31) != 0;  // (int32) term negative: sign-extends into the high word
+    if (!(b & 0x80u)) break;
+  }
+  pos += k + 1;
+  val = COMPAT ? (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32) : (int64_t)spec;
+  return true;
+}
+
+template <bool COMPAT>
+__device__ __forceinline__ bool fast_list_gather(const FastSrc& s, const DevOut& o, uint32_t kind, uint32_t lo,
+                                                 uint32_t ll, uint64_t dst) {
+  uint32_t q = lo;
+  const uint32_t le = lo + ll;
+  while (q < le) {
+    uint32_t fn, co, cl;
+    if (!ffield(s, q, le, fn, co, cl) || fn != 1u) return false;
+    if (kind == TFRG_KIND_BYTES) {
+      if (dst < o.cap_b) {
+        o.b_off[dst] = (uint32_t)(s.base + co);
+        o.b_len[dst] = cl;
+      }
+      ++dst;
+    } else if (kind == TFRG_KIND_FLOAT) {
+      if (cl & 3u) return false;
+      for (uint32_t i = 0; i < cl; i += 4) {
+        if (dst < o.cap_f32) o.f32[dst] = lds_u32u(s.l, s.p + co + i);
+        ++dst;
+      }
+    } else {
+      uint32_t p = co;
+      const uint32_t e = co + cl;
+      while (p < e) {
+        int64_t v;
+        if (!fast_value<COMPAT>(s, p, e, v)) return false;
+        if (dst < o.cap_i64) o.i64[dst] = v;
+        ++dst;
+      }
+    }
+  }
+  return true;
+}
+
 template <bool COMPAT, class S>
 __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t r,
                                               S& s) {
@@ -1172,9 +1253,18 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
     }
     if (mine) {
       if (staged) {
+        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
         LdsSrc s;
         s.init(stage, lo16, v.p0, v.L);
-        gather_record<COMPAT>(B, sc, o, r, s);
+        for (uint32_t k = 0; k < sc.n_slots; ++k) {
+          const size_t at = (size_t)k * B.n + r;
+          if (!o.order[at]) continue;
+          const uint2 lc = o.loc[at];
+          const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+          const uint32_t kind = sc.slot_kind[k];
+          if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
+            list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+        }
       } else {
         Src s;
         s.init(B.bytes, v.p0, v.L);
@@ -1240,8 +1330,10 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   mark(kStageScan);
   if (sc.n_slots > 0) {
     const uint32_t n_tiles = (b.n + kScanTile - 1) / kScanTile;
-    hipLaunchKernelGGL(k_scan, dim3(n_tiles * sc.n_slots), dim3(kScanBlock), 0, st, o.count, o.rs, o.totals,
-                       o.granules, o.ticket, o.info, b.n, n_tiles);
+    const dim3 grid(n_tiles, sc.n_slots);
+    hipLaunchKernelGGL(k_scan_reduce, grid, dim3(kScanBlock), 0, st, o.count, o.tsum, b.n, n_tiles);
+    hipLaunchKernelGGL(k_scan_spine, dim3(sc.n_slots), dim3(kScanBlock), 0, st, o.tsum, o.totals, n_tiles);
+    hipLaunchKernelGGL(k_scan_down, grid, dim3(kScanBlock), 0, st, o.count, o.rs, o.tsum, o.totals, b.n, n_tiles);
   }
   mark(kStageBase);
   hipLaunchKernelGGL(k_base, dim3(1), dim3(64), 0, st, o.totals, sc.slot_kind, o.slot_base, o.kind_totals,
