@@ -568,7 +568,7 @@ constexpr int kWavesPerBlock = kWaveBlock / 64;
 __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int status, int64_t aux,
                                               uint32_t verdict) {
   o.status[r] = status;
-  o.aux[r] = aux;
+  if (status != TFRG_OK) o.aux[r] = aux;  // aux is defined only for failing records
   o.verdict[r] = (uint8_t)verdict;
   if (status == TFRG_ST_SCHEMA_MISS) {
     atomicAdd(&o.info[kInfoMissRecords], 1u);
@@ -602,6 +602,27 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t x) {
     x = y > x ? y : x;
   }
   return x;
+}
+
+// Span [lo, hi) covering the records of the lanes with `in` set. Whole-file batches are ascending
+// and contiguous, so the first / last participating lanes bound it; one ballot verifies that and
+// the 64-bit shuffle reductions run only when it does not hold.
+__device__ __forceinline__ void wave_span(bool in, uint64_t a, uint64_t b, uint64_t& lo, uint64_t& hi) {
+  const uint64_t m = __ballot(in);
+  if (!m) {
+    lo = ~0ull;
+    hi = 0;
+    return;
+  }
+  const int f = __builtin_ctzll(m), l = 63 - __builtin_clzll(m);
+  const uint64_t lo_c = __shfl(a, f, 64), hi_c = __shfl(b, l, 64);
+  if (__ballot(in && (a < lo_c || b > hi_c)) == 0) {
+    lo = lo_c;
+    hi = hi_c;
+    return;
+  }
+  lo = wave_min_u64(in ? a : ~0ull);
+  hi = wave_max_u64(in ? b : 0ull);
 }
 
 // LDS writes of one wave made visible to its other lanes
@@ -685,15 +706,40 @@ __device__ __forceinline__ bool fv32(const FastSrc& s, uint32_t& pos, uint32_t& 
   return true;
 }
 
-// a length-delimited field inside [pos, end): returns its field number, payload offset and length
+// a length-delimited field inside [pos, end): returns its field number, payload offset and length.
+// Common case: 1-byte tag + 1..3-byte length, decoded from ONE 4-byte stage read.
 __device__ __forceinline__ bool ffield(const FastSrc& s, uint32_t& pos, uint32_t end, uint32_t& fn, uint32_t& off,
                                        uint32_t& len) {
-  uint32_t key;
-  if (!fv32(s, pos, key) || (key & 7u) != 2u) return false;
-  fn = key >> 3;
-  if (!fv32(s, pos, len) || pos > end || len > end - pos) return false;
-  off = pos;
-  pos += len;
+  if (pos > s.L) return false;
+  const uint32_t w = s.w4(pos);
+  if ((w & 0x87u) != 0x02u) {  // tag longer than 1 byte, or not wire type 2
+    uint32_t key;
+    if (!fv32(s, pos, key) || (key & 7u) != 2u) return false;
+    fn = key >> 3;
+    if (!fv32(s, pos, len) || pos > end || len > end - pos) return false;
+    off = pos;
+    pos += len;
+    return true;
+  }
+  fn = (w & 0x7fu) >> 3;
+  uint32_t l, hb;
+  if (!(w & 0x8000u)) {
+    l = (w >> 8) & 0x7fu;
+    hb = 2;
+  } else if (!(w & 0x800000u)) {
+    l = ((w >> 8) & 0x7fu) | ((w >> 9) & 0x3f80u);
+    hb = 3;
+  } else if (!(w & 0x80000000u)) {
+    l = ((w >> 8) & 0x7fu) | ((w >> 9) & 0x3f80u) | ((w >> 10) & 0x1fc000u);
+    hb = 4;
+  } else {
+    return false;
+  }
+  const uint32_t q = pos + hb;
+  if (q > end || l > end - q) return false;
+  off = q;
+  len = l;
+  pos = q + l;
   return true;
 }
 
@@ -1092,10 +1138,21 @@ __global__ __launch_bounds__(kScanBlock) void k_scan_down(const uint32_t* __rest
   uint32_t total;
   uint32_t run = tsum[(size_t)slot * n_tiles + tile] + block_excl_scan(sum, s_w, total);
   uint32_t* out = rs + (size_t)slot * (n + 1);
+  uint32_t w[kScanItems];
 #pragma unroll
   for (int i = 0; i < kScanItems; ++i) {
-    if (base + i < n) out[base + i] = run;
+    w[i] = run;
     run += v[i];
+  }
+  const uint64_t gaddr = (size_t)slot * (n + 1) + base;  // element index of out[base] in rs
+  if (base + kScanItems <= n && (gaddr & 3u) == 0) {
+#pragma unroll
+    for (int i = 0; i < kScanItems; i += 4)
+      *reinterpret_cast<uint4*>(out + base + i) = make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < kScanItems; ++i)
+      if (base + i < n) out[base + i] = w[i];
   }
   if (tile == 0 && threadIdx.x == 0) out[n] = totals[slot];
 }
@@ -1243,8 +1300,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
       v = rec_view(B, r);
       mine = v.status == TFRG_OK && v.e - v.st <= lane_max && o.status[r] == TFRG_OK;
     }
-    const uint64_t lo = wave_min_u64(mine ? v.st : ~0ull);
-    const uint64_t hi = wave_max_u64(mine ? v.e : 0ull);
+    uint64_t lo, hi;
+    wave_span(mine, v.st, v.e, lo, hi);
     const uint64_t lo16 = lo & ~15ull;
     const bool staged = hi > lo && hi - lo16 <= kStageBytes;
     if (staged) {
@@ -1256,14 +1313,29 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
         const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
         LdsSrc s;
         s.init(stage, lo16, v.p0, v.L);
-        for (uint32_t k = 0; k < sc.n_slots; ++k) {
-          const size_t at = (size_t)k * B.n + r;
-          if (!o.order[at]) continue;
-          const uint2 lc = o.loc[at];
-          const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
-          const uint32_t kind = sc.slot_kind[k];
-          if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
-            list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+        for (uint32_t k0 = 0; k0 < sc.n_slots; k0 += 4) {
+          // issue every slot's metadata loads up front (no load waits on another)
+          uint32_t ordv[4], rsv[4];
+          uint2 lcv[4];
+          uint64_t basev[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t k = k0 + j < sc.n_slots ? k0 + j : k0;
+            const size_t at = (size_t)k * B.n + r;
+            ordv[j] = o.order[at];
+            lcv[j] = o.loc[at];
+            rsv[j] = o.rs[(size_t)k * (B.n + 1) + r];
+            basev[j] = o.slot_base[k];
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t k = k0 + j;
+            if (k >= sc.n_slots || !ordv[j]) continue;
+            const uint32_t kind = sc.slot_kind[k];
+            const uint64_t dst = basev[j] + rsv[j];
+            if (!fast_list_gather<COMPAT>(fs, o, kind, lcv[j].x, lcv[j].y, dst))
+              list_gather<COMPAT>(s, o, (int)kind, (int64_t)lcv[j].x, (int64_t)lcv[j].y, dst);
+          }
         }
       } else {
         Src s;

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--files", type=int, default=256)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--lane-max", type=int, default=None)
+    ap.add_argument("--no-crc", action="store_true")
     a = ap.parse_args()
     sample, (big, st, en) = workload(a.config, a.files)
     dev = torch.device("cuda", 0)
@@ -47,7 +48,8 @@ def main():
     s = torch.cuda.current_stream(dev)
     dec.set_profiling(True)
     for _ in range(a.iters):
-        dec.decode_device(d_b.data_ptr(), big.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0], stream=s.cuda_stream)
+        dec.decode_device(d_b.data_ptr(), big.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0], stream=s.cuda_stream,
+                          crc=not a.no_crc)
         print({k: round(v, 4) for k, v in dec.profile_last().items()}, flush=True)
     info = dec.info()
     print("errors", info.n_errors, "miss", info.n_miss_records, "big", info.n_big, "bytes", big.size, "records", st.shape[0])
