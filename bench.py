@@ -42,23 +42,43 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--files", type=int, default=FILES_PER_GPU, help="C1 files (x65,536 records) per GPU")
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
+                    help="c1 (default, configs[1]); c2 flowers-shaped; c3 wide schema")
+    ap.add_argument("--files", type=int, default=None, help="replicas of the base file per GPU")
     ap.add_argument("--profile-steps", type=int, default=5)
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
-def build_shard(rank: int, files: int):
-    """Framed C1 image of one file (seeded by rank) replicated `files` times."""
+CONFIGS = {
+    # name: (default replicas of the base file per GPU, description)
+    "c1": (FILES_PER_GPU, "C1 (configs[1]): {files} files x 65536 records per GPU, int64 label + 12 B bytes_list id"),
+    "c2": (1, "C2 (configs[2]): oxford_flowers102-shaped, {files} x 8189 records per GPU, lognormal image bytes"),
+    "c3": (16, "C3 (configs[3]): wide schema 32 int64_list + 32 float_list, {files} x 8192 records per GPU"),
+}
+
+
+def base_payloads(config: str, rank: int) -> list[bytes]:
     from tfr_reader import synth
 
-    pl = synth.c1_payloads(RECORDS_PER_FILE, offset=rank * RECORDS_PER_FILE)
+    if config == "c1":
+        return synth.c1_payloads(RECORDS_PER_FILE, offset=rank * RECORDS_PER_FILE)
+    if config == "c2":
+        return synth.c2_payloads(8189, seed=2 + rank)
+    return synth.c3_payloads(8192, seed=3 + rank)
+
+
+def build_shard(rank: int, config: str, files: int):
+    """Framed base file (seeded by rank) replicated `files` times."""
+    from tfr_reader import synth
+
+    pl = base_payloads(config, rank)
     buf, st, en = synth.framed(pl, crc=True)
     return (buf, st, en), synth.replicate(buf, st, en, files)
 
 
-def cpu_baseline(sample, seconds: float) -> dict:
+def cpu_baseline(sample, seconds: float, config: str = "c1") -> dict:
     """Oracle decode (restated reference algorithm, C) of the sample on host threads."""
     from oracle import oracle as O
 
@@ -89,7 +109,7 @@ def cpu_baseline(sample, seconds: float) -> dict:
         "examples_per_s": r / wall,
         "cores": cores,
         "kind": "port",
-        "sample": f"one C1 file ({st.shape[0]} records, {nbytes / 2**20:.2f} MiB) decoded repeatedly by "
+        "sample": f"one {config.upper()} file ({st.shape[0]} records, {nbytes / 2**20:.2f} MiB) decoded repeatedly by "
         f"{cores} threads for {seconds:.1f} s wall ({cores * seconds:.0f} core-s)",
     }
 
@@ -111,7 +131,8 @@ def main() -> None:
 
     from tfr_reader import hip
 
-    sample, (big, st, en) = build_shard(rank, args.files)
+    files = args.files if args.files is not None else CONFIGS[args.config][0]
+    sample, (big, st, en) = build_shard(rank, args.config, files)
     n = int(st.shape[0])
     nbytes = int(big.size)
     framed_bytes = int((en - st).sum())
@@ -134,7 +155,8 @@ def main() -> None:
     torch.cuda.synchronize(dev)
     info = dec.info()
     assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0, "decode check failed"
-    assert info.kind_totals[3] == n and info.kind_totals[1] == n, "value totals"
+    if args.config == "c1":
+        assert info.kind_totals[3] == n and info.kind_totals[1] == n, "value totals"
 
     # ---- timed region
     if dist:
@@ -171,18 +193,29 @@ def main() -> None:
     kern_ms = {k: float(np.mean(v)) for k, v in per.items()}
     dominant = max(kern_ms, key=kern_ms.get)
 
-    # algorithmic bytes: k_lane_count reads every framed byte plus the two
-    # u64 offsets and writes the u32 status of each record.
+    # algorithmic bytes per launch. Count kernels (lane / wave) read every
+    # framed byte of their records plus the two u64 offsets and write the u32 status; gather
+    # kernels write the values (8 B int64, 4 B float, 8 B bytes view) and one u32 row split per
+    # (slot, record).
+    n_slots = len(dec.keys.slot_key)
+    n_big = int(info.n_big)
+    big_bytes = 0
+    if n_big:
+        sz = (en - st)
+        big_bytes = int(sz[sz > hip.DEFAULT_LANE_MAX].sum())
+    small_bytes = framed_bytes - big_bytes
+    vals = 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 8 * int(info.kind_totals[1])
     alg = {
-        "k_lane_count": framed_bytes + 16 * n + 4 * n,
-        # k_lane_gather re-reads each present list and writes the values: label int64 (8 B) and
-        # the id view (8 B), reading order/loc/row-splits of both slots (2 x (2+8+4) B)
-        "k_lane_gather": n * (2 * 14 + 8 + 8),
+        "k_lane_count": small_bytes + 20 * (n - n_big),
+        "k_wave_count": big_bytes + 20 * n_big,
+        "k_lane_gather": vals + 4 * n * n_slots,
+        "k_wave_gather": vals + 4 * n * n_slots,
+        "k_scan": 12 * n * n_slots,
     }
     a_bytes = alg.get(dominant, framed_bytes + 20 * n)
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
     # whole-pipeline algorithmic bytes: R + W
-    n_keys = 2
+    n_keys = len(dec.keys.keys)
     R = framed_bytes + 16 * n
     W = 4 * n + 4 * n * n_keys + 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 12 * int(info.kind_totals[1])
 
@@ -193,7 +226,7 @@ def main() -> None:
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(sample, args.cpu_seconds)
+        cpu = cpu_baseline(sample, args.cpu_seconds, args.config)
 
     if dist:
         tdist.barrier()
@@ -214,8 +247,7 @@ def main() -> None:
             "dtype": "u8",
             "data": "synthetic",
             "config": {
-                "workload": f"C1 (configs[1]): {args.files} files x {RECORDS_PER_FILE} records per GPU, "
-                "int64 label + 12 B bytes_list id, spec CRC-32C, resident in HBM",
+                "workload": CONFIGS[args.config][1].format(files=files) + ", spec CRC-32C, resident in HBM",
                 "records_per_gpu": n,
                 "framed_bytes_per_gpu": framed_bytes,
                 "parallelism": f"file-sharded x{world} (no collective on the data path)",

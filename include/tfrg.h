@@ -68,7 +68,7 @@ typedef struct tfrg_ctx tfrg_ctx;
 
 int tfrg_ctx_create(int device, tfrg_ctx** out);
 int tfrg_ctx_destroy(tfrg_ctx* ctx);
-/* records larger than lane_max bytes take the wavefront-per-record kernels (default 16384) */
+/* records larger than lane_max bytes take the wavefront-per-record kernels (default 2048) */
 int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
 
 /* Per-kernel timing: with profiling on, every decode records HIP events on its stream around

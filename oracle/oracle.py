@@ -39,7 +39,9 @@ def lib() -> C.CDLL:
                                     C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
         L.oracle_decode_framed.restype = C.c_int64
         L.oracle_decode_framed.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int64, C.c_int,
-                                           C.c_void_p]
+                                           C.c_int, C.c_void_p]
+        L.oracle_crc32c_fast.restype = C.c_uint32
+        L.oracle_crc32c_fast.argtypes = [C.c_void_p, C.c_uint64]
         L.oracle_index.restype = C.c_int64
         L.oracle_index.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_int64]
         L.oracle_crc32c.restype = C.c_uint32
@@ -117,11 +119,16 @@ def masked_crc32c(data: bytes) -> int:
     return int(lib().oracle_masked_crc32c(a.ctypes.data, len(data)))
 
 
-def decode_framed_bulk(buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, compat: bool = True):
-    """CPU baseline: decode framed records; returns (status array, total value count)."""
+def crc32c_fast(data: bytes) -> int:
+    a = np.frombuffer(data or b"\0", np.uint8)
+    return int(lib().oracle_crc32c_fast(a.ctypes.data, len(data)))
+
+
+def decode_framed_bulk(buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, compat: bool = True, crc: bool = True):
+    """CPU baseline: CRC verdicts + reference decode of framed records; (status array, work count)."""
     st = np.ascontiguousarray(starts, np.uint64)
     en = np.ascontiguousarray(ends, np.uint64)
     status = np.zeros(st.shape[0], np.int32)
     total = lib().oracle_decode_framed(buf.ctypes.data, buf.size, st.ctypes.data, en.ctypes.data, st.shape[0],
-                                       int(compat), status.ctypes.data)
+                                       int(compat), int(crc), status.ctypes.data)
     return status, total

@@ -67,7 +67,7 @@ def test_golden_cases_bit_exact(dec, lane_max):
     try:
         r = dec.decode(*payload_batch(payloads), payload_only=True)
     finally:
-        dec.set_lane_max(16384)
+        dec.set_lane_max(hip.DEFAULT_LANE_MAX)
     bad = []
     for i, c in enumerate(cases):
         st, aux = int(r.status[i]), int(r.aux[i])
@@ -162,7 +162,7 @@ def test_lane_and_wave_kernels_agree(dec, lane_max):
     try:
         other = dec.decode(buf, st, en)
     finally:
-        dec.set_lane_max(16384)
+        dec.set_lane_max(hip.DEFAULT_LANE_MAX)
     for name in ("status", "verdict", "order", "row_splits", "i64", "f32", "bytes_off", "bytes_len"):
         assert np.array_equal(getattr(base, name), getattr(other, name)), name
 

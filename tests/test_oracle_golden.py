@@ -122,3 +122,20 @@ def test_crc32c_rfc3720_vectors():
     assert O.crc32c(bytes(range(31, -1, -1))) == 0x113FDB5C
     assert O.masked_crc32c(struct.pack("<Q", 18)) == 0x25641F24
     assert O.masked_crc32c(b"") == 0xA282EAD8
+
+
+def test_table_crc_matches_bitwise():
+    import random
+
+    rng = random.Random(5)
+    for n in [0, 1, 7, 8, 9, 63, 64, 1000]:
+        data = bytes(rng.getrandbits(8) for _ in range(n))
+        assert O.crc32c_fast(data) == O.crc32c(data)
+
+
+def test_bulk_baseline_counts_crcs():
+    from tfr_reader import synth
+
+    buf, st, en = synth.framed(synth.c1_payloads(100))
+    status, work = O.decode_framed_bulk(buf, st, en)
+    assert not status.any() and work == 100 * 2 + 100 * 2  # two CRC matches + two values each

@@ -61,7 +61,7 @@ struct tfrg_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
   hipStream_t last_stream = nullptr;
-  uint32_t lane_max = 16384;
+  uint32_t lane_max = 2048;
   int num_cus = 256;
   // constants
   DBuf crc_tab, consts;

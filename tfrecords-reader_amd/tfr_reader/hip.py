@@ -20,6 +20,9 @@ from tfr_reader import _native as N
 from tfr_reader import _status as S
 
 KIND_NAMES = {1: "bytes_list", 2: "float_list", 3: "int64_list"}
+
+#: records larger than this (framed bytes) are decoded one wavefront per record (libtfrg default)
+DEFAULT_LANE_MAX = 2048
 KIND_IDS = {v: k for k, v in KIND_NAMES.items()}
 
 
