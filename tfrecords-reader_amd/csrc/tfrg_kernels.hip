@@ -632,7 +632,7 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// copy absolute bytes [lo16, hi) (lo16 16-aligned, hi - lo16 <= kStageBytes) into dst
+// copy absolute bytes [lo16, hi) (lo16 16-aligned) into dst
 __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
                                            uint32_t lane) {
   // four 1 KiB wave-loads in flight per round, held in named registers (no scratch)
@@ -995,28 +995,116 @@ __global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSch
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Wavefront-per-record kernels for records above lane_max. A record that fits kWStage is staged
+// into the wave's LDS (coalesced 16 B loads), CRC'd from LDS by all 64 lanes, and walked in two
+// phases: the Features level is walked once (wave-uniform) to list the map entries, then each
+// lane parses its own entries (key lookup, Feature, list validation + count) — the per-entry work
+// that dominates wide schemas runs 64-wide. Anything non-canonical falls back to the exact walker.
+// Larger records keep the streaming CRC and the wave-uniform exact walk from HBM.
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave
+constexpr uint32_t kWStageStride = kWStage + 64;
+constexpr uint32_t kMaxEnt = 256;                   // map entries per record on the parallel path
+
+// wave CRC-32C of stage bytes [a, b) (stage offsets, a/b arbitrary), same algebra as crc_wave
+__device__ uint32_t crc_wave_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<1>& T, const uint32_t* A,
+                                 const uint32_t* consts, uint32_t lane) {
+  const uint32_t c0 = a >> 4, c1 = (b - 1) >> 4;
+  const uint32_t nch = c1 - c0 + 1;
+  const int32_t rounds = (int32_t)((nch + 63) >> 6);
+  uint32_t S = 0;
+  for (int32_t k = rounds - 1; k >= 0; --k) {
+    const int32_t ch = (int32_t)c1 - 64 * k - (int32_t)lane;
+    uint32_t Rc = 0;
+    if (ch >= (int32_t)c0) {
+      const uint32_t q = (uint32_t)ch << 4;
+      const uint4 w = *reinterpret_cast<const uint4*>(l + q);
+      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+      if (q < a + 4 || q + 16 > b) {
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+          uint32_t keep = 0, inv = 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t ba = q + 4u * k2 + j;
+            if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
+            if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
+          }
+          ws[k2] = (ws[k2] & keep) ^ inv;
+        }
+      }
+#pragma unroll
+      for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
+    }
+    S = A[S & 0xffu] ^ A[256 + ((S >> 8) & 0xffu)] ^ A[512 + ((S >> 16) & 0xffu)] ^ A[768 + (S >> 24)] ^ Rc;
+  }
+  uint32_t t = gf_mul(S, consts[lane]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
+  const uint32_t z = 16u * (c1 + 1) - b;
+  t = gf_mul(t, consts[64 + z]);
+  return ~t;
+}
+
+// Phase B of the parallel walk for one entry: fills slot/rank-free results; false = bail.
+__device__ __forceinline__ bool entry_fast(const FastSrc& s, const LdsKeys& K, uint32_t eo, uint32_t el, int& kid,
+                                           int& slot, uint32_t& lo, uint32_t& ll, uint32_t& cnt) {
+  uint32_t e = eo;
+  const uint32_t ee = eo + el;
+  uint32_t kn, ko, kl, vn, vo, vl, kind, g;
+  if (!ffield(s, e, ee, kn, ko, kl) || kn != 1u) return false;
+  if (!ffield(s, e, ee, vn, vo, vl) || vn != 2u || e != ee) return false;
+  kid = fast_lookup(s, K, ko, kl);
+  if (kid < 0) return false;
+  g = vo;
+  if (!ffield(s, g, vo + vl, kind, lo, ll) || g != vo + vl || kind < 1u || kind > 3u) return false;
+  if (!fast_list_count(s, kind, lo, ll, cnt)) return false;
+  slot = (int)K.rec[(uint32_t)kid * kKrWords + kKrSlot1 + kind - 1];
+  return slot >= 0;
+}
+
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
                                                           const uint32_t* __restrict__ crc_tab,
                                                           const uint32_t* __restrict__ consts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;          // [4][256] slice-by-4
-  uint32_t* A = lds + 1024;     // [4][256] (x) x^8192
-  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 2048);  // [waves][n_slots]
+  uint32_t* tab = lds;       // [4][256] slice-by-4
+  uint32_t* A = lds + 1024;  // [4][256] (x) x^8192
+  uint32_t* kht = lds + 2048;
+  uint32_t* krec = kht + kLdsMaxHt;
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
+  uint8_t* per_wave = reinterpret_cast<uint8_t*>(krec + kLdsMaxKeys * kKrWords);
+  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * 2u + 15u) & ~15u);
+  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes;
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = per_wave + wib * wave_bytes;
+  uint32_t* ent = reinterpret_cast<uint32_t*>(stage + kWStageStride);  // (len << 16) | off
+  uint32_t* kmark = reinterpret_cast<uint32_t*>(ent + kMaxEnt);
+  uint16_t* word = reinterpret_cast<uint16_t*>(kmark + kLdsMaxKeys);
   for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
+  if (fast_ok) {
+    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
+  }
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  const LdsKeys K{kht, krec, sc.ht_mask};
   const uint32_t nbig = o.info[kInfoBig];
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-  uint16_t* word = ord + wib * sc.n_slots;
 
   for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
     const uint32_t r = o.big_list[i];
     RecView v = rec_view(B, r);
     int64_t aux = 0;
     CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
+    const uint64_t lo16 = v.st & ~15ull;
+    const bool staged = v.e - lo16 <= kWStage;
+    if (staged) {
+      stage_span(stage, B.bytes, lo16, v.e, lane);
+      wave_lds_sync();
+    }
     if (framed) {
       const uint64_t D = v.e - v.st;
       if (D >= 8) {
@@ -1028,22 +1116,90 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
         }
         if (do_crc && D >= 16) {
           const uint64_t a = v.p0, b = v.e - 4;
-          const uint32_t c = (b - a >= 64) ? crc_wave(B.bytes, a, b, T, A, consts, lane)
-                                           : crc_serial<1>(B.bytes, a, b, T);
+          uint32_t c;
+          if (b - a < 64) c = crc_serial<1>(B.bytes, a, b, T);
+          else if (staged) c = crc_wave_lds(stage, (uint32_t)(a - lo16), (uint32_t)(b - lo16), T, A, consts, lane);
+          else c = crc_wave(B.bytes, a, b, T, A, consts, lane);
           if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
         }
       }
     }
     for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
-    __builtin_amdgcn_wave_barrier();
-    Src s;
-    s.init(B.bytes, v.p0, v.L);
-    int status = walk_example<COMPAT>(s, sink, aux);
-    if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-    __builtin_amdgcn_wave_barrier();
-    sink.finalize(status == TFRG_OK);
+    wave_lds_sync();
+    int status = kBail;
+    if (staged && fast_ok) {
+      // phase A (wave-uniform): the single Features field and its map entries
+      const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+      bool ok = true, have = false;
+      uint32_t n_ent = 0, pos = 0;
+      while (ok && pos < fs.L) {
+        uint32_t fn, fo, fl;
+        if (have || !ffield(fs, pos, fs.L, fn, fo, fl) || fn != 1u) {
+          ok = false;
+          break;
+        }
+        have = true;
+        uint32_t q = fo;
+        while (q < fo + fl) {
+          uint32_t en, eo, el;
+          if (n_ent >= kMaxEnt || !ffield(fs, q, fo + fl, en, eo, el) || en != 1u) {
+            ok = false;
+            break;
+          }
+          if (lane == 0) ent[n_ent] = (el << 16) | eo;
+          ++n_ent;
+        }
+      }
+      ok = ok && have;
+      for (uint32_t k = lane; k < sc.n_keys; k += 64) kmark[k] = 0;
+      wave_lds_sync();
+      // phase B (64-wide): one entry per lane
+      bool lane_ok = true;
+      if (ok) {
+        for (uint32_t j = lane; j < n_ent; j += 64) {
+          const uint32_t en = ent[j];
+          int kid = -1, slot = -1;
+          uint32_t lo = 0, ll = 0, cnt = 0;
+          if (!entry_fast(fs, K, en & 0xffffu, en >> 16, kid, slot, lo, ll, cnt) ||
+              atomicAdd(&kmark[kid], 1u) != 0u) {  // duplicate key: exact path
+            lane_ok = false;
+            continue;
+          }
+          sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(j + 1);  // rank = entry position
+          const size_t at = (size_t)slot * B.n + r;
+          o.count[at] = cnt;
+          o.loc[at] = make_uint2(lo, ll);
+        }
+      }
+      wave_lds_sync();
+      if (ok && __ballot(!lane_ok) == 0 && n_ent < 65535u) status = TFRG_OK;
+    }
+    if (status == kBail) {  // exact, wave-uniform walk (from the stage when staged)
+      for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
+      wave_lds_sync();
+      sink.rank = 0;
+      if (staged) {
+        LdsSrc s;
+        s.init(stage, lo16, v.p0, v.L);
+        status = walk_example<COMPAT>(s, sink, aux);
+      } else {
+        Src s;
+        s.init(B.bytes, v.p0, v.L);
+        status = walk_example<COMPAT>(s, sink, aux);
+      }
+      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+    }
+    wave_lds_sync();
+    // finalize, one slot per lane
+    const bool good = status == TFRG_OK;
+    for (uint32_t k = lane; k < sc.n_slots; k += 64) {
+      const uint32_t vv = good ? sink.ord[(size_t)k * sink.ostride] : 0u;
+      const size_t at = (size_t)k * B.n + r;
+      o.order[at] = (uint16_t)vv;
+      if (!vv) o.count[at] = 0;
+    }
     if (lane == 0) record_result(o, r, status, aux, v.verdict);
-    __builtin_amdgcn_wave_barrier();
+    wave_lds_sync();
   }
 }
 
@@ -1349,15 +1505,40 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
 
 template <bool COMPAT>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchema sc, DevOut o) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
   const uint32_t nbig = o.info[kInfoBig];
   for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
     const uint32_t r = o.big_list[i];
-    if (lane != 0 || o.status[r] != TFRG_OK) continue;
+    if (o.status[r] != TFRG_OK) continue;  // wave-uniform
     const RecView v = rec_view(B, r);
-    Src s;
-    s.init(B.bytes, v.p0, v.L);
-    gather_record<COMPAT>(B, sc, o, r, s);
+    const uint64_t lo16 = v.st & ~15ull;
+    const bool staged = v.e - lo16 <= kWStage;
+    if (staged) {
+      stage_span(stage, B.bytes, lo16, v.e, lane);
+      wave_lds_sync();
+    }
+    for (uint32_t k = lane; k < sc.n_slots; k += 64) {
+      const size_t at = (size_t)k * B.n + r;
+      if (!o.order[at]) continue;
+      const uint2 lc = o.loc[at];
+      const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+      const uint32_t kind = sc.slot_kind[k];
+      if (staged) {
+        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+        if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst)) {
+          LdsSrc s;
+          s.init(stage, lo16, v.p0, v.L);
+          list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+        }
+      } else {
+        Src s;
+        s.init(B.bytes, v.p0, v.L);
+        list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+      }
+    }
+    wave_lds_sync();
   }
 }
 
@@ -1382,7 +1563,10 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
                               ? (kLdsMaxHt + (size_t)sc.n_keys * kKrWords) * 4 : 0;
   const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds + keys_lds;
-  const size_t wave_lds = 2048ull * 4 + (size_t)sc.n_slots * kWavesPerBlock * 2;
+  const size_t wave_shared = (2048ull + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
+  const size_t wave_per = (size_t)kWStageStride + kMaxEnt * 4 + kLdsMaxKeys * 4;
+  const size_t wave_lds = wave_shared + kWavesPerBlock * (wave_per + (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15));
+  const size_t wave_lds_g = wave_shared + kWavesPerBlock * wave_per;
   mark(kStageLaneCount);
   if (lane_lds <= kLdsBudget) {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
@@ -1396,7 +1580,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o,
                        d_tab, d_consts);
   } else {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b, sc,
+    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds_g, st, b, sc,
                        o, d_tab, d_consts);
   }
   mark(kStageScan);
@@ -1417,7 +1601,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   }
   mark(kStageWaveGather);
   if (sc.n_slots > 0) {
-    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
+    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock),
+                       (size_t)kWStageStride * kWavesPerBlock, st, b, sc, o);
   }
   mark(kNumStages);
   return hipGetLastError();
