@@ -70,6 +70,9 @@ int tfrg_ctx_create(int device, tfrg_ctx** out);
 int tfrg_ctx_destroy(tfrg_ctx* ctx);
 /* records larger than lane_max bytes take the wavefront-per-record kernels (default 2048) */
 int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
+/* wavefront records spanning <= nbytes are staged in LDS (clamped to the kernel's 12 KiB stage;
+ * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
+int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
 
 /* Per-kernel timing: with profiling on, every decode records HIP events on its stream around
  * each kernel stage; tfrg_profile_last waits for the last decode and writes up to cap stage

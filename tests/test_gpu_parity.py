@@ -57,17 +57,20 @@ def payload_batch(payloads):
     return b"".join(payloads), ends - lens, ends
 
 
-@pytest.mark.parametrize("lane_max", [1 << 20, 0])
-def test_golden_cases_bit_exact(dec, lane_max):
+@pytest.mark.parametrize("lane_max,wave_stage", [(1 << 20, 1 << 20), (0, 1 << 20), (0, 0)])
+def test_golden_cases_bit_exact(dec, lane_max, wave_stage):
     """Every reference case (valid, malformed, fuzzed) in one device batch; lane_max=0 forces the
-    wavefront-per-record kernels, 1 MiB the lane-per-record kernels."""
+    wavefront-per-record kernels (LDS-staged, or streaming with wave_stage=0), 1 MiB the
+    lane-per-record kernels."""
     cases = G.load_cases()
     payloads = [bytes.fromhex(c["payload"]) for c in cases]
     dec.set_lane_max(lane_max)
+    dec.set_wave_stage(wave_stage)
     try:
         r = dec.decode(*payload_batch(payloads), payload_only=True)
     finally:
         dec.set_lane_max(hip.DEFAULT_LANE_MAX)
+        dec.set_wave_stage(1 << 20)
     bad = []
     for i, c in enumerate(cases):
         st, aux = int(r.status[i]), int(r.aux[i])
@@ -153,16 +156,18 @@ def test_c3_shape_vs_oracle(dec, orc):
     assert not _compare_to_oracle(r, orc, buf, st, en)
 
 
-@pytest.mark.parametrize("lane_max", [0, 1 << 20])
-def test_lane_and_wave_kernels_agree(dec, lane_max):
+@pytest.mark.parametrize("lane_max,wave_stage", [(0, 1 << 20), (0, 0), (1 << 20, 1 << 20)])
+def test_lane_and_wave_kernels_agree(dec, lane_max, wave_stage):
     pl = synth.c3_payloads(64, seed=11) + synth.c1_payloads(300) + synth.c2_payloads(8, seed=4, scale=0.1)
     buf, st, en = synth.framed(pl)
     base = dec.decode(buf, st, en)
     dec.set_lane_max(lane_max)
+    dec.set_wave_stage(wave_stage)
     try:
         other = dec.decode(buf, st, en)
     finally:
         dec.set_lane_max(hip.DEFAULT_LANE_MAX)
+        dec.set_wave_stage(1 << 20)
     for name in ("status", "verdict", "order", "row_splits", "i64", "f32", "bytes_off", "bytes_len"):
         assert np.array_equal(getattr(base, name), getattr(other, name)), name
 

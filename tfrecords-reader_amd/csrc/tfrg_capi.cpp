@@ -62,6 +62,7 @@ struct tfrg_ctx {
   hipStream_t own_stream = nullptr;
   hipStream_t last_stream = nullptr;
   uint32_t lane_max = 2048;
+  uint32_t wave_stage = 0xffffffffu;  // clamped to the kernel's stage size
   int num_cus = 256;
   // constants
   DBuf crc_tab, consts;
@@ -145,6 +146,12 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
 int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
   if (!c) return TFRG_E_ARG;
   c->lane_max = lane_max;
+  return 0;
+}
+
+int tfrg_ctx_set_wave_stage(tfrg_ctx* c, uint32_t nbytes) {
+  if (!c) return TFRG_E_ARG;
+  c->wave_stage = nbytes;
   return 0;
 }
 
@@ -336,6 +343,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   const uint64_t wave_blocks = (n + 3) / 4;
   cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
   cfg.lane_max = c->lane_max;
+  cfg.wave_stage = c->wave_stage;
   if (n) {
     hipEvent_t* ev = nullptr;
     if (c->profiling) {
@@ -400,7 +408,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->first_error = h[kInfoFirstError];
   info->n_miss_records = h[kInfoMissRecords];
   info->n_miss_entries = h[kInfoMissEntries];
-  info->n_big = h[kInfoBig];
+  info->n_big = h[kInfoBig] + h[kInfoHuge];
   info->scan_timeout = h[kInfoScanTimeout];
   for (int k = 0; k < 4; ++k) info->kind_totals[k] = kt[k];
   info->nbytes = c->nbytes;

@@ -55,6 +55,7 @@ enum InfoIdx : uint32_t {
   kInfoMissEntries = 3,  // miss entries appended (may exceed capacity)
   kInfoBig = 4,          // records routed to the wave-per-record kernels
   kInfoScanTimeout = 5,  // reserved (always 0: the scan has no inter-workgroup waits)
+  kInfoHuge = 6,         // wave records too large for the LDS stage (listed from the end of big_list)
   kInfoCount = 16
 };
 
@@ -95,6 +96,7 @@ struct LaunchCfg {
   int lane_grid;
   int wave_grid;
   uint32_t lane_max;       // records above this size go to the wave kernels
+  uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).

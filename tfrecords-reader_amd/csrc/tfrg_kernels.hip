@@ -25,6 +25,20 @@
 
 namespace tfrg {
 
+// Optional per-phase cycle accounting of the wavefront kernels (make prof -> libtfrg_prof.so);
+// compiled out of the product library.
+#ifdef TFRG_PHASE_PROF
+__device__ unsigned long long g_phase[16];
+#define PHASE_MARK(t) const uint64_t t = __builtin_readcyclecounter()
+#define PHASE_ADD(i, a, b) \
+  do {                     \
+    if (lane == 0) atomicAdd(&g_phase[i], (unsigned long long)((b) - (a))); \
+  } while (0)
+#else
+#define PHASE_MARK(t) (void)0
+#define PHASE_ADD(i, a, b) (void)0
+#endif
+
 // ------------------------------------------------------------------------------------------------
 // Byte source: payload bytes of one record with the reference's out-of-range behaviour
 // (index == L reads the CPython NUL terminator, index > L is reference UB), read through a
@@ -531,9 +545,8 @@ struct RecView {
   uint32_t verdict;
 };
 
-__device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
+__device__ __forceinline__ RecView rec_view_se(const DevBatch& B, uint64_t st, uint64_t en) {
   RecView v;
-  const uint64_t st = B.start[r], en = B.end[r];
   v.st = st;
   v.status = TFRG_OK;
   v.verdict = 0;
@@ -556,6 +569,10 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
     v.L = (int64_t)(v.e - st);
   }
   return v;
+}
+
+__device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
+  return rec_view_se(B, B.start[r], B.end[r]);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -625,12 +642,18 @@ __device__ __forceinline__ void wave_span(bool in, uint64_t a, uint64_t b, uint6
   hi = wave_max_u64(in ? b : 0ull);
 }
 
-// LDS writes of one wave made visible to its other lanes
+// Memory writes of one wave made visible to its other lanes. A wavefront's memory instructions
+// are processed in order, so wavefront scope needs no waits (workgroup scope would drain every
+// outstanding global store, a multi-microsecond stall per call); this orders the compiler only.
 __device__ __forceinline__ void wave_lds_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave (wavefront kernels)
+constexpr uint32_t kWStageStride = kWStage + 64;
+constexpr uint32_t kMaxEnt = 256;                   // map entries per record on the parallel path
 
 // copy absolute bytes [lo16, hi) (lo16 16-aligned) into dst
 __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
@@ -932,7 +955,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
 template <int R, bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
-                                                           uint32_t lane_max) {
+                                                           uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;                                           // 1024 * R dwords
   uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 1024 * R);   // [n_slots][kLaneBlock]
@@ -963,9 +986,14 @@ __global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSch
     if (valid) {
       v = rec_view(B, r);
       const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
-      if (big) {  // large record: wavefront kernel
-        const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
-        o.big_list[i] = r;
+      if (big) {  // large record: wavefront kernels (staged ones from the front, huge from the back)
+        if (v.e - (v.st & ~15ull) <= wave_stage) {
+          const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
+          o.big_list[i] = r;
+        } else {
+          const uint32_t i = atomicAdd(&o.info[kInfoHuge], 1u);
+          o.big_list[B.n - 1u - i] = r;
+        }
       }
       mine = !big;
     }
@@ -1003,9 +1031,6 @@ __global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSch
 // that dominates wide schemas runs 64-wide. Anything non-canonical falls back to the exact walker.
 // Larger records keep the streaming CRC and the wave-uniform exact walk from HBM.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave
-constexpr uint32_t kWStageStride = kWStage + 64;
-constexpr uint32_t kMaxEnt = 256;                   // map entries per record on the parallel path
 
 // wave CRC-32C of stage bytes [a, b) (stage offsets, a/b arbitrary), same algebra as crc_wave
 __device__ uint32_t crc_wave_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<1>& T, const uint32_t* A,
@@ -1047,6 +1072,31 @@ __device__ uint32_t crc_wave_lds(const uint8_t* l, uint32_t a, uint32_t b, const
   return ~t;
 }
 
+// Scalar read of a canonical length-delimited field-1 header at `q`: tag 0x0a + length varint of
+// <= 3 bytes; sets the body offset/length (body inside the payload) or returns false (bail).
+__device__ __forceinline__ bool hdr_0a(const FastSrc& s, uint32_t q, uint32_t& bo, uint32_t& bl) {
+  if (q + 2 > s.L) return false;
+  const uint32_t w = __builtin_amdgcn_readfirstlane(s.w4(q));
+  if ((w & 0xffu) != 0x0au) return false;
+  const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
+  uint32_t h, len;
+  if (b1 < 0x80u) {
+    h = 2;
+    len = b1;
+  } else if (b2 < 0x80u) {
+    h = 3;
+    len = (b1 & 0x7fu) | (b2 << 7);
+  } else if (b3 < 0x80u) {
+    h = 4;
+    len = (b1 & 0x7fu) | ((b2 & 0x7fu) << 7) | (b3 << 14);
+  } else {
+    return false;
+  }
+  bo = q + h;
+  bl = len;
+  return bo <= s.L && len <= s.L - bo;
+}
+
 // Phase B of the parallel walk for one entry: fills slot/rank-free results; false = bail.
 __device__ __forceinline__ bool entry_fast(const FastSrc& s, const LdsKeys& K, uint32_t eo, uint32_t el, int& kid,
                                            int& slot, uint32_t& lo, uint32_t& ll, uint32_t& cnt) {
@@ -1064,6 +1114,19 @@ __device__ __forceinline__ bool entry_fast(const FastSrc& s, const LdsKeys& K, u
   return slot >= 0;
 }
 
+// Finalize of a wavefront record: order/count columns, one slot per lane.
+template <class Sink>
+__device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink, uint32_t n_slots, uint32_t n,
+                                              uint32_t r, bool good, uint32_t lane) {
+  for (uint32_t k = lane; k < n_slots; k += 64) {
+    const uint32_t vv = good ? sink.ord[(size_t)k * sink.ostride] : 0u;
+    const size_t at = (size_t)k * n + r;
+    o.order[at] = (uint16_t)vv;
+    if (!vv) o.count[at] = 0;
+  }
+}
+
+// Huge records (beyond the LDS stage): streaming CRC from HBM and the wave-uniform exact walk.
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
                                                           const uint32_t* __restrict__ crc_tab,
@@ -1071,40 +1134,20 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;       // [4][256] slice-by-4
   uint32_t* A = lds + 1024;  // [4][256] (x) x^8192
-  uint32_t* kht = lds + 2048;
-  uint32_t* krec = kht + kLdsMaxHt;
-  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
-  uint8_t* per_wave = reinterpret_cast<uint8_t*>(krec + kLdsMaxKeys * kKrWords);
-  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * 2u + 15u) & ~15u);
-  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes;
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
-  uint8_t* stage = per_wave + wib * wave_bytes;
-  uint32_t* ent = reinterpret_cast<uint32_t*>(stage + kWStageStride);  // (len << 16) | off
-  uint32_t* kmark = reinterpret_cast<uint32_t*>(ent + kMaxEnt);
-  uint16_t* word = reinterpret_cast<uint16_t*>(kmark + kLdsMaxKeys);
+  const uint32_t ord_words = (sc.n_slots + 7u) / 8u * 4u;
+  uint16_t* word = reinterpret_cast<uint16_t*>(lds + 2048 + wib * ord_words);
   for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
-  if (fast_ok) {
-    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
-    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
-  }
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  const LdsKeys K{kht, krec, sc.ht_mask};
-  const uint32_t nbig = o.info[kInfoBig];
+  const uint32_t nhuge = o.info[kInfoHuge];
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-
-  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
-    const uint32_t r = o.big_list[i];
+  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nhuge; i += gridDim.x * kWavesPerBlock) {
+    const uint32_t r = o.big_list[B.n - 1u - i];
     RecView v = rec_view(B, r);
     int64_t aux = 0;
     CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
-    const uint64_t lo16 = v.st & ~15ull;
-    const bool staged = v.e - lo16 <= kWStage;
-    if (staged) {
-      stage_span(stage, B.bytes, lo16, v.e, lane);
-      wave_lds_sync();
-    }
     if (framed) {
       const uint64_t D = v.e - v.st;
       if (D >= 8) {
@@ -1116,41 +1159,166 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
         }
         if (do_crc && D >= 16) {
           const uint64_t a = v.p0, b = v.e - 4;
-          uint32_t c;
-          if (b - a < 64) c = crc_serial<1>(B.bytes, a, b, T);
-          else if (staged) c = crc_wave_lds(stage, (uint32_t)(a - lo16), (uint32_t)(b - lo16), T, A, consts, lane);
-          else c = crc_wave(B.bytes, a, b, T, A, consts, lane);
+          const uint32_t c = b - a < 64 ? crc_serial<1>(B.bytes, a, b, T) : crc_wave(B.bytes, a, b, T, A, consts, lane);
           if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
         }
       }
     }
     for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
     wave_lds_sync();
+    Src s;
+    s.init(B.bytes, v.p0, v.L);
+    int status = walk_example<COMPAT>(s, sink, aux);
+    if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+    wave_lds_sync();
+    wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
+    if (lane == 0) record_result(o, r, status, aux, v.verdict);
+    wave_lds_sync();
+  }
+}
+
+// Software pipeline of the staged wavefront kernels: the next record's bytes are loaded into
+// registers (12 x 16 B per lane) while the current one is walked from LDS, so HBM latency hides
+// behind the walk. Loads are unconditional (clamped addresses) so the wait counts stay static.
+constexpr int kPrefWords = (int)(kWStage / 1024);
+struct Pref {  // named fields, returned by value: an array or an out-parameter is kept in scratch
+  uint4 w0, w1, w2, w3, w4, w5, w6, w7, w8, w9, w10, w11;
+};
+
+#define TFRG_PREF_LOAD(j)                                                        \
+  {                                                                              \
+    const uint64_t q = lo16 + lane * 16u + (uint32_t)(j)*1024u;                  \
+    p.w##j = *reinterpret_cast<const uint4*>(src + (q < hi ? q : 0ull));          \
+  }
+#define TFRG_PREF_STORE(j)                                                       \
+  {                                                                              \
+    const uint32_t off = lane * 16u + (uint32_t)(j) * 1024u;                     \
+    if (lo16 + off < hi) *reinterpret_cast<uint4*>(dst + off) = p.w##j;          \
+  }
+
+__device__ __forceinline__ Pref pref_load_v(const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  Pref p;
+  static_assert(kPrefWords == 12, "pref_load is spelled out for 12 words");
+  TFRG_PREF_LOAD(0) TFRG_PREF_LOAD(1) TFRG_PREF_LOAD(2) TFRG_PREF_LOAD(3) TFRG_PREF_LOAD(4) TFRG_PREF_LOAD(5)
+  TFRG_PREF_LOAD(6) TFRG_PREF_LOAD(7) TFRG_PREF_LOAD(8) TFRG_PREF_LOAD(9) TFRG_PREF_LOAD(10) TFRG_PREF_LOAD(11)
+  return p;
+}
+
+__device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  TFRG_PREF_STORE(0) TFRG_PREF_STORE(1) TFRG_PREF_STORE(2) TFRG_PREF_STORE(3) TFRG_PREF_STORE(4)
+  TFRG_PREF_STORE(5) TFRG_PREF_STORE(6) TFRG_PREF_STORE(7) TFRG_PREF_STORE(8) TFRG_PREF_STORE(9)
+  TFRG_PREF_STORE(10) TFRG_PREF_STORE(11)
+}
+#undef TFRG_PREF_LOAD
+#undef TFRG_PREF_STORE
+
+// Medium records (lane_max < size, span <= kWStage): staged in LDS; CRC from LDS by all lanes;
+// the Features level walked once with scalar loads to list the map entries, then one entry per
+// lane (key lookup, Feature, list validation + count); anything else -> exact walk from LDS.
+template <bool COMPAT, bool GORD>
+__global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchema sc, DevOut o,
+                                                           const uint32_t* __restrict__ crc_tab,
+                                                           const uint32_t* __restrict__ consts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  uint32_t* tab = lds;         // [4][256] slice-by-4
+  uint32_t* A = lds + 1024;    // [4][256] (x) x^8192
+  uint32_t* cst = lds + 2048;  // [128] combine / unshift constants
+  uint32_t* kht = cst + 128;
+  uint32_t* krec = kht + kLdsMaxHt;
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
+  uint8_t* per_wave = reinterpret_cast<uint8_t*>(krec + kLdsMaxKeys * kKrWords);
+  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * 2u + 15u) & ~15u);
+  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes;
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = per_wave + wib * wave_bytes;
+  uint32_t* ent = reinterpret_cast<uint32_t*>(stage + kWStageStride);  // (len << 16) | off
+  uint32_t* kmark = reinterpret_cast<uint32_t*>(ent + kMaxEnt);
+  uint16_t* word = reinterpret_cast<uint16_t*>(kmark + kLdsMaxKeys);
+  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
+  for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
+  if (fast_ok) {
+    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
+  }
+  __syncthreads();
+  const LdsTab<1> T{tab, 0};
+  const LdsKeys K{kht, krec, sc.ht_mask};
+  const uint32_t nbig = o.info[kInfoBig];
+  const bool framed = !(B.flags & kFlagPayloadOnly);
+  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
+
+  // pipeline state: record i+stride (r1: bytes in flight) and i+2*stride (r2: start/end in flight)
+  uint32_t r1 = 0, r2 = 0;
+  uint64_t s1 = 0, e1 = 0, s2 = 0, e2 = 0;
+  Pref pf;
+  if (i < nbig) {
+    r1 = o.big_list[i];
+    s1 = B.start[r1];
+    e1 = B.end[r1];
+  }
+  pf = pref_load_v(B.bytes, s1 & ~15ull, e1 < B.nbytes ? e1 : B.nbytes, lane);
+  if (i + stride < nbig) {
+    r2 = o.big_list[i + stride];
+    s2 = B.start[r2];
+    e2 = B.end[r2];
+  }
+  for (; i < nbig; i += stride) {
+    const uint32_t r = r1;
+    const uint64_t en_raw = e1;
+    RecView v = rec_view_se(B, s1, e1);
+    const uint64_t lo16 = v.st & ~15ull;
+    pref_store(pf, stage, lo16, v.e, lane);
+    wave_lds_sync();
+    r1 = r2;
+    s1 = s2;
+    e1 = e2;
+    const bool more2 = i + 2 * stride < nbig;
+    if (more2) r2 = o.big_list[i + 2 * stride];
+    pf = pref_load_v(B.bytes, s1 & ~15ull, i + stride < nbig ? (e1 < B.nbytes ? e1 : B.nbytes) : 0ull, lane);
+    if (more2) {
+      s2 = B.start[r2];
+      e2 = B.end[r2];
+    }
+
+    int64_t aux = 0;
+    CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
+    if (framed) {
+      const uint64_t D = v.e - v.st;
+      const uint32_t o0 = (uint32_t)(v.st - lo16);
+      if (D >= 8) {
+        const uint64_t lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
+        if (lenf == en_raw - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+        if (do_crc && D >= 12) {
+          const uint32_t c = crc_lds<1>(stage, o0, o0 + 8, T);
+          if (crc_mask(c) == lds_u32u(stage, o0 + 8)) v.verdict |= TFRG_V_LEN_CRC;
+        }
+        if (do_crc && D >= 16) {
+          const uint32_t a = o0 + 12, b = (uint32_t)(v.e - lo16) - 4;
+          const uint32_t c = b - a < 64 ? crc_lds<1>(stage, a, b, T) : crc_wave_lds(stage, a, b, T, A, cst, lane);
+          if (crc_mask(c) == lds_u32u(stage, b)) v.verdict |= TFRG_V_DATA_CRC;
+        }
+      }
+    }
+    for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
+    wave_lds_sync();
     int status = kBail;
-    if (staged && fast_ok) {
-      // phase A (wave-uniform): the single Features field and its map entries
+    if (fast_ok) {
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-      bool ok = true, have = false;
-      uint32_t n_ent = 0, pos = 0;
-      while (ok && pos < fs.L) {
-        uint32_t fn, fo, fl;
-        if (have || !ffield(fs, pos, fs.L, fn, fo, fl) || fn != 1u) {
+      // phase A (scalar): the single Features field and its map entries
+      uint32_t n_ent = 0, fo = 0, fl = 0;
+      bool ok = hdr_0a(fs, 0, fo, fl) && fo + fl == fs.L;
+      for (uint32_t q = fo; ok && q < fs.L;) {
+        uint32_t eo, el;
+        if (n_ent >= kMaxEnt || !hdr_0a(fs, q, eo, el)) {
           ok = false;
           break;
         }
-        have = true;
-        uint32_t q = fo;
-        while (q < fo + fl) {
-          uint32_t en, eo, el;
-          if (n_ent >= kMaxEnt || !ffield(fs, q, fo + fl, en, eo, el) || en != 1u) {
-            ok = false;
-            break;
-          }
-          if (lane == 0) ent[n_ent] = (el << 16) | eo;
-          ++n_ent;
-        }
+        if (lane == 0) ent[n_ent] = (el << 16) | eo;
+        ++n_ent;
+        q = eo + el;
       }
-      ok = ok && have;
       for (uint32_t k = lane; k < sc.n_keys; k += 64) kmark[k] = 0;
       wave_lds_sync();
       // phase B (64-wide): one entry per lane
@@ -1172,32 +1340,19 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
         }
       }
       wave_lds_sync();
-      if (ok && __ballot(!lane_ok) == 0 && n_ent < 65535u) status = TFRG_OK;
+      if (ok && __ballot(!lane_ok) == 0) status = TFRG_OK;
     }
-    if (status == kBail) {  // exact, wave-uniform walk (from the stage when staged)
+    if (status == kBail) {  // exact, wave-uniform walk from the stage
       for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
       wave_lds_sync();
       sink.rank = 0;
-      if (staged) {
-        LdsSrc s;
-        s.init(stage, lo16, v.p0, v.L);
-        status = walk_example<COMPAT>(s, sink, aux);
-      } else {
-        Src s;
-        s.init(B.bytes, v.p0, v.L);
-        status = walk_example<COMPAT>(s, sink, aux);
-      }
+      LdsSrc s;
+      s.init(stage, lo16, v.p0, v.L);
+      status = walk_example<COMPAT>(s, sink, aux);
       if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
     }
     wave_lds_sync();
-    // finalize, one slot per lane
-    const bool good = status == TFRG_OK;
-    for (uint32_t k = lane; k < sc.n_slots; k += 64) {
-      const uint32_t vv = good ? sink.ord[(size_t)k * sink.ostride] : 0u;
-      const size_t at = (size_t)k * B.n + r;
-      o.order[at] = (uint16_t)vv;
-      if (!vv) o.count[at] = 0;
-    }
+    wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
     if (lane == 0) record_result(o, r, status, aux, v.verdict);
     wave_lds_sync();
   }
@@ -1503,40 +1658,140 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
   }
 }
 
+// Huge records: one slot per lane, lists read from HBM.
 template <bool COMPAT>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchema sc, DevOut o) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
-  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
-  const uint32_t nbig = o.info[kInfoBig];
-  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
-    const uint32_t r = o.big_list[i];
+  const uint32_t nhuge = o.info[kInfoHuge];
+  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nhuge; i += gridDim.x * kWavesPerBlock) {
+    const uint32_t r = o.big_list[B.n - 1u - i];
     if (o.status[r] != TFRG_OK) continue;  // wave-uniform
     const RecView v = rec_view(B, r);
-    const uint64_t lo16 = v.st & ~15ull;
-    const bool staged = v.e - lo16 <= kWStage;
-    if (staged) {
-      stage_span(stage, B.bytes, lo16, v.e, lane);
-      wave_lds_sync();
-    }
     for (uint32_t k = lane; k < sc.n_slots; k += 64) {
       const size_t at = (size_t)k * B.n + r;
       if (!o.order[at]) continue;
       const uint2 lc = o.loc[at];
       const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
-      const uint32_t kind = sc.slot_kind[k];
-      if (staged) {
-        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-        if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst)) {
-          LdsSrc s;
-          s.init(stage, lo16, v.p0, v.L);
-          list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
-        }
-      } else {
-        Src s;
-        s.init(B.bytes, v.p0, v.L);
-        list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+      Src s;
+      s.init(B.bytes, v.p0, v.L);
+      list_gather<COMPAT>(s, o, (int)sc.slot_kind[k], (int64_t)lc.x, (int64_t)lc.y, dst);
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int k) {
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, k);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), k);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Values of up to 64 slots of one staged record (one slot per lane). Canonical packed float lists
+// are copied by the whole wave (lane j moves value j: contiguous stores); int64 and bytes lists
+// and anything non-canonical are decoded by their own lane.
+template <bool COMPAT>
+__device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevOut& o, bool present, uint32_t kind,
+                                                   uint2 lc, uint64_t dst, uint64_t lo16, uint32_t lane) {
+  bool fail = false;
+  uint64_t m = __ballot(present && kind == TFRG_KIND_FLOAT && lc.y != 0u);
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint32_t lo = __builtin_amdgcn_readlane(lc.x, k), ll = __builtin_amdgcn_readlane(lc.y, k);
+    const uint64_t d = readlane_u64(dst, k);
+    uint32_t bo, bl;
+    if (!hdr_0a(fs, lo, bo, bl) || bo + bl != lo + ll || (bl & 3u)) {
+      fail |= lane == (uint32_t)k;
+      continue;
+    }
+    const uint32_t cnt = bl >> 2;
+    for (uint32_t j = lane; j < cnt; j += 64) {
+      if (d + j < o.cap_f32) o.f32[d + j] = lds_u32u(fs.l, fs.p + bo + 4u * j);
+    }
+  }
+  if (present && (kind != TFRG_KIND_FLOAT || fail)) {
+    if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst)) {
+      LdsSrc s;
+      s.init(fs.l, lo16, fs.base, fs.L);
+      list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+    }
+  }
+}
+
+// Medium records: staged in LDS with the same register pipeline as k_stage_count.
+template <bool COMPAT>
+__global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSchema sc, DevOut o) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t lane = threadIdx.x & 63u, wib = threadIdx.x >> 6;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
+  const uint32_t nbig = o.info[kInfoBig];
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
+  uint32_t r1 = 0, r2 = 0;
+  uint64_t s1 = 0, e1 = 0, s2 = 0, e2 = 0;
+  int st1 = -1, st2 = -1;
+  Pref pf;
+  if (i < nbig) {
+    r1 = o.big_list[i];
+    s1 = B.start[r1];
+    e1 = B.end[r1];
+    st1 = o.status[r1];
+  }
+  pf = pref_load_v(B.bytes, s1 & ~15ull, st1 == TFRG_OK ? (e1 < B.nbytes ? e1 : B.nbytes) : 0ull, lane);
+  if (i + stride < nbig) {
+    r2 = o.big_list[i + stride];
+    s2 = B.start[r2];
+    e2 = B.end[r2];
+    st2 = o.status[r2];
+  }
+  for (; i < nbig; i += stride) {
+    const uint32_t r = r1;
+    const bool ok = st1 == TFRG_OK;
+    const RecView v = rec_view_se(B, s1, e1);
+    const uint64_t lo16 = v.st & ~15ull;
+    if (ok) pref_store(pf, stage, lo16, v.e, lane);
+    wave_lds_sync();
+    // slot metadata of this record (issued ahead of the next record's byte loads)
+    bool present = false;
+    uint32_t kind = 0;
+    uint2 lc = make_uint2(0, 0);
+    uint64_t dst = 0;
+    if (ok && lane < sc.n_slots) {
+      const size_t at = (size_t)lane * B.n + r;
+      present = o.order[at] != 0;
+      lc = o.loc[at];
+      dst = o.slot_base[lane] + o.rs[(size_t)lane * (B.n + 1) + r];
+      kind = sc.slot_kind[lane];
+    }
+    r1 = r2;
+    s1 = s2;
+    e1 = e2;
+    st1 = st2;
+    const bool more2 = i + 2 * stride < nbig;
+    if (more2) r2 = o.big_list[i + 2 * stride];
+    pf = pref_load_v(B.bytes, s1 & ~15ull,
+              (i + stride < nbig && st1 == TFRG_OK) ? (e1 < B.nbytes ? e1 : B.nbytes) : 0ull, lane);
+    if (more2) {
+      s2 = B.start[r2];
+      e2 = B.end[r2];
+      st2 = o.status[r2];
+    }
+    if (!ok) continue;  // wave-uniform
+    const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+    stage_gather_group<COMPAT>(fs, o, present, kind, lc, dst, lo16, lane);
+    for (uint32_t kb = 64; kb < sc.n_slots; kb += 64) {  // wide schemas: further groups of 64 slots
+      const uint32_t k = kb + lane;
+      bool pk = false;
+      uint32_t kk = 0;
+      uint2 lk = make_uint2(0, 0);
+      uint64_t dk = 0;
+      if (k < sc.n_slots) {
+        const size_t at = (size_t)k * B.n + r;
+        pk = o.order[at] != 0;
+        lk = o.loc[at];
+        dk = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+        kk = sc.slot_kind[k];
       }
+      stage_gather_group<COMPAT>(fs, o, pk, kk, lk, dk, lo16, lane);
     }
     wave_lds_sync();
   }
@@ -1563,25 +1818,38 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
                               ? (kLdsMaxHt + (size_t)sc.n_keys * kKrWords) * 4 : 0;
   const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds + keys_lds;
-  const size_t wave_shared = (2048ull + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
+  const size_t wave_shared = (2048ull + 128 + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
   const size_t wave_per = (size_t)kWStageStride + kMaxEnt * 4 + kLdsMaxKeys * 4;
-  const size_t wave_lds = wave_shared + kWavesPerBlock * (wave_per + (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15));
-  const size_t wave_lds_g = wave_shared + kWavesPerBlock * wave_per;
+  const size_t stage_lds_w =
+      wave_shared + kWavesPerBlock * (wave_per + (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15));
+  const size_t stage_lds_wg = wave_shared + kWavesPerBlock * wave_per;
+  const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
   mark(kStageLaneCount);
   if (lane_lds <= kLdsBudget) {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
-                       b, sc, o, d_tab, cfg.lane_max);
+                       b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else {
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock),
-                       tab_lds + stage_lds + keys_lds, st, b, sc, o, d_tab, cfg.lane_max);
+                       tab_lds + stage_lds + keys_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageWaveCount);
-  if (wave_lds <= kLdsBudget) {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds, st, b, sc, o,
-                       d_tab, d_consts);
+  // staged (record span <= kWStage) and huge records: two launches, the second with a small LDS
+  // footprint so the streaming CRC of huge records runs at full occupancy
+  const size_t ord_lds = kWavesPerBlock * (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15);
+  const size_t huge_lds = 2048ull * 4 + ord_lds;
+  if (stage_lds_w <= kLdsBudget) {
+    hipLaunchKernelGGL((k_stage_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_w, st, b,
+                       sc, o, d_tab, d_consts);
   } else {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), wave_lds_g, st, b, sc,
+    hipLaunchKernelGGL((k_stage_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_wg, st, b,
+                       sc, o, d_tab, d_consts);
+  }
+  if (huge_lds <= kLdsBudget) {
+    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), huge_lds, st, b, sc,
                        o, d_tab, d_consts);
+  } else {
+    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b,
+                       sc, o, d_tab, d_consts);
   }
   mark(kStageScan);
   if (sc.n_slots > 0) {
@@ -1601,8 +1869,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   }
   mark(kStageWaveGather);
   if (sc.n_slots > 0) {
-    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock),
+    hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock),
                        (size_t)kWStageStride * kWavesPerBlock, st, b, sc, o);
+    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
   }
   mark(kNumStages);
   return hipGetLastError();
@@ -1615,3 +1884,15 @@ hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o
 }
 
 }  // namespace tfrg
+
+#ifdef TFRG_PHASE_PROF
+extern "C" int tfrg_debug_phase(unsigned long long* out, int n, int reset) {
+  if (n > 16) n = 16;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tfrg::g_phase), n * sizeof(unsigned long long)) != hipSuccess) return -2;
+  if (reset) {
+    unsigned long long z[16] = {};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tfrg::g_phase), z, sizeof(z)) != hipSuccess) return -2;
+  }
+  return n;
+}
+#endif

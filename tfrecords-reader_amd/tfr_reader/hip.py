@@ -98,6 +98,10 @@ class HipDecoder:
     def set_lane_max(self, nbytes: int) -> None:
         N.check(self._lib.tfrg_ctx_set_lane_max(self._ctx, nbytes), "tfrg_ctx_set_lane_max")
 
+    def set_wave_stage(self, nbytes: int) -> None:
+        """Records above lane_max spanning <= nbytes go to the LDS-staged wavefront kernels."""
+        N.check(self._lib.tfrg_ctx_set_wave_stage(self._ctx, nbytes), "tfrg_ctx_set_wave_stage")
+
     def set_profiling(self, on: bool) -> None:
         N.check(self._lib.tfrg_ctx_set_profiling(self._ctx, int(on)), "tfrg_ctx_set_profiling")
 

@@ -4,11 +4,15 @@
 usage: prof_decode.py [--config c1|c2|c3] [--files N] [--iters K]
 """
 import argparse
+import ctypes
+import os
 import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
 sys.path[:0] = [str(REPO / "tfrecords-reader_amd"), str(REPO)]
+if "--phase" in sys.argv:  # per-phase cycle counters of the wavefront kernels (make -C csrc prof)
+    os.environ["TFRG_LIB"] = str(REPO / "tfrecords-reader_amd" / "tfr_reader" / "libtfrg_prof.so")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -34,6 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--lane-max", type=int, default=None)
     ap.add_argument("--no-crc", action="store_true")
+    ap.add_argument("--phase", action="store_true")
     a = ap.parse_args()
     sample, (big, st, en) = workload(a.config, a.files)
     dev = torch.device("cuda", 0)
@@ -45,12 +50,28 @@ def main():
     if a.lane_max is not None:
         dec.set_lane_max(a.lane_max)
     dec.decode(*sample)
+    if a.phase:
+        from tfr_reader import _native
+
+        (ctypes.c_ulonglong * 16)()
+        _native.lib().tfrg_debug_phase((ctypes.c_ulonglong * 16)(), 16, 1)
     s = torch.cuda.current_stream(dev)
     dec.set_profiling(True)
     for _ in range(a.iters):
         dec.decode_device(d_b.data_ptr(), big.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0], stream=s.cuda_stream,
                           crc=not a.no_crc)
         print({k: round(v, 4) for k, v in dec.profile_last().items()}, flush=True)
+    if a.phase:
+        from tfr_reader import _native
+
+        L = _native.lib()
+        arr = (ctypes.c_ulonglong * 16)()
+        L.tfrg_debug_phase(arr, 16, 1)
+        names = ["w.stage", "w.crc", "w.zero", "w.phaseA", "w.phaseB", "w.exact", "w.final", "w.total",
+                 "w.bails", "g.stage", "g.slots"]
+        tot = arr[7] or 1
+        for i, nm in enumerate(names):
+            print(f"{nm:10s} {arr[i]:>16d} {arr[i] / tot:8.3f}")
     info = dec.info()
     print("errors", info.n_errors, "miss", info.n_miss_records, "big", info.n_big, "bytes", big.size, "records", st.shape[0])
 
