@@ -219,6 +219,54 @@ def main() -> None:
     R = framed_bytes + 16 * n
     W = 4 * n + 4 * n * n_keys + 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 12 * int(info.kind_totals[1])
 
+    # ---- achievable HBM read bandwidth on this box: streaming read of the batch
+    from tfr_reader import _native
+
+    L = _native.lib()
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    rd_bytes = (nbytes // 16) * 16
+
+    def stream_read():
+        _native.check(L.tfrg_stream_read(d_bytes.data_ptr(), rd_bytes, sink.data_ptr(), stream.cuda_stream),
+                      "tfrg_stream_read")
+
+    for _ in range(3):
+        stream_read()
+    s0 = torch.cuda.Event(enable_timing=True)
+    s1 = torch.cuda.Event(enable_timing=True)
+    s0.record(stream)
+    for _ in range(10):
+        stream_read()
+    s1.record(stream)
+    torch.cuda.synchronize(dev)
+    hbm_read_gbs = rd_bytes * 10 / (s0.elapsed_time(s1) / 1e3) / 1e9
+
+    # ---- single-batch figure: one base file resident, one decode, HIP events
+    sb_buf, sb_st, sb_en = sample
+    d_sb = torch.zeros(((sb_buf.size + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
+    d_sb[: sb_buf.size].copy_(torch.from_numpy(sb_buf))
+    d_sbs = torch.from_numpy(sb_st.view(np.int64)).to(dev)
+    d_sbe = torch.from_numpy(sb_en.view(np.int64)).to(dev)
+    sb_n = int(sb_st.shape[0])
+
+    def single():
+        dec.decode_device(d_sb.data_ptr(), sb_buf.size, d_sbs.data_ptr(), d_sbe.data_ptr(), sb_n,
+                          stream=stream.cuda_stream)
+
+    for _ in range(3):
+        single()
+    sb_ms = []
+    for _ in range(10):
+        a0 = torch.cuda.Event(enable_timing=True)
+        a1 = torch.cuda.Event(enable_timing=True)
+        a0.record(stream)
+        single()
+        a1.record(stream)
+        torch.cuda.synchronize(dev)
+        sb_ms.append(a0.elapsed_time(a1))
+    sb_ms = float(np.median(sb_ms))
+    sb_bytes = int((sb_en - sb_st).sum())
+
     ms_step = elapsed / args.steps * 1e3
     gib_s_rank = framed_bytes / (ms_step / 1e3) / 2**30
     value = framed_bytes * world / (elapsed / args.steps) / 2**30
@@ -263,6 +311,14 @@ def main() -> None:
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
                 "traffic": None,
                 "algorithmic_bytes_per_launch": a_bytes,
+                "achievable_read_GBps": round(hbm_read_gbs, 1),
+            },
+            "single_batch": {
+                "records": sb_n,
+                "framed_bytes": sb_bytes,
+                "ms": round(sb_ms, 4),
+                "GiB_s": round(sb_bytes / (sb_ms / 1e3) / 2**30, 3),
+                "examples_per_s": round(sb_n / (sb_ms / 1e3), 1),
             },
             "pipeline": {
                 "alg_bytes_R_plus_W": R + W,

@@ -139,6 +139,11 @@ int tfrg_result_device(tfrg_ctx* ctx, tfrg_columns* cols);
 /* copy the last result into caller host buffers sized from tfrg_info; NULL members are skipped */
 int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);
 
+/* Measurement helper (achievable HBM read bandwidth next to the 8 TB/s spec): one
+ * streaming read of d_bytes[0, nbytes) (16 B loads, nbytes a multiple of 16) on `stream`, XOR-folded
+ * into the u32 at d_sink so the loads are live. Not part of the decode path. */
+int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -458,3 +458,9 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
 }
 
 }  // extern "C"
+
+int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream) {
+  if (!d_bytes || !d_sink || (nbytes & 15u)) return TFRG_E_ARG;
+  return tfrg::launch_stream_read(d_bytes, nbytes, d_sink, static_cast<hipStream_t>(stream)) == hipSuccess
+             ? 0 : TFRG_E_HIP;
+}

@@ -68,6 +68,7 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tfrg_ctx_set_lane_max": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_wave_stage": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "tfrg_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_profile_last": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
     "tfrg_set_schema": (

@@ -67,8 +67,8 @@ def main():
         L = _native.lib()
         arr = (ctypes.c_ulonglong * 16)()
         L.tfrg_debug_phase(arr, 16, 1)
-        names = ["w.stage", "w.crc", "w.zero", "w.phaseA", "w.phaseB", "w.exact", "w.final", "w.total",
-                 "w.bails", "g.stage", "g.slots"]
+        names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
+                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane"]
         tot = arr[7] or 1
         for i, nm in enumerate(names):
             print(f"{nm:10s} {arr[i]:>16d} {arr[i] / tot:8.3f}")
