@@ -59,6 +59,9 @@ enum InfoIdx : uint32_t {
   kInfoCount = 16
 };
 
+// count column: bit 31 set = the slot's single value is stored inline in the loc word
+constexpr uint32_t kCountInline = 0x80000000u;
+
 struct DevOut {
   int32_t* status;       // [n]
   int64_t* aux;          // [n] error detail

@@ -415,6 +415,7 @@ struct CountSink {
       rk = ++rank;
     }
     ord[(size_t)slot * ostride] = (uint16_t)rk;
+    if (count & kCountInline) return TFRG_ST_LIMIT;  // >= 2^31 values in one list
     if (leader) {
       const size_t at = (size_t)slot * n + r;
       o->count[at] = count;
@@ -423,7 +424,7 @@ struct CountSink {
     return TFRG_OK;
   }
 
-  __device__ void finalize(bool ok) {
+  __device__ __forceinline__ void finalize(bool ok) {
     for (uint32_t k = 0; k < sc->n_slots; ++k) {
       const uint32_t v = ok ? ord[(size_t)k * ostride] : 0u;
       if (leader) {
@@ -579,6 +580,9 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // Kernels
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
+#ifndef TFRG_LANE_MINB
+#define TFRG_LANE_MINB 4  // workgroups per CU the count kernel is register-budgeted for
+#endif
 constexpr int kWaveBlock = 256;
 constexpr int kWavesPerBlock = kWaveBlock / 64;
 
@@ -842,7 +846,74 @@ __device__ __forceinline__ int fast_lookup(const FastSrc& s, const LdsKeys& K, u
 }
 
 // Returns TFRG_OK with the dict in sink.ord / count / loc, or kBail.
-__device__ int fast_walk(const FastSrc& s, const LdsKeys& K, CountSink& sink) {
+template <bool COMPAT>
+__device__ __forceinline__ bool fast_value(const FastSrc& s, uint32_t& pos, uint32_t e, int64_t& val) {
+  const uint32_t w = s.w4(pos);
+  const uint32_t term = ~w & 0x80808080u;
+  if (term) {
+    const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
+    if (pos + nb > e) return false;
+    const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+    val = (int64_t)(x & ((1u << (7u * nb)) - 1u));
+    pos += nb;
+    return true;
+  }
+  // 5..10 bytes: two more words, terminator found by bit scan, groups combined branch-free (no
+  // dependent byte-at-a-time chain: a long varint costs one extra LDS round trip)
+  const uint32_t w1 = s.w4s(pos + 4), w2 = s.w4s(pos + 8);
+  const uint32_t t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
+  uint32_t nb;
+  if (t1) nb = 5u + (__builtin_ctz(t1) >> 3);
+  else if (t2) nb = 9u + (__builtin_ctz(t2) >> 3);
+  else return false;  // > 10 bytes: "Too many bytes when decoding varint." (exact path)
+  if (pos + nb > e) return false;
+  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+  const uint32_t g4 = w1 & 0x7fu;
+  const uint32_t g5 = nb > 5u ? (w1 >> 8) & 0x7fu : 0u;
+  const uint32_t g6 = nb > 6u ? (w1 >> 16) & 0x7fu : 0u;
+  const uint32_t g7 = nb > 7u ? (w1 >> 24) & 0x7fu : 0u;
+  const uint32_t g8 = nb > 8u ? w2 & 0x7fu : 0u;
+  const uint32_t g9 = nb > 9u ? (w2 >> 8) & 0x7fu : 0u;
+  pos += nb;
+  if (COMPAT) {  // term_k = (int32)(g_k << (7k & 31)), sign-extended, OR-ed (decoder.pyx:34-50)
+    const uint32_t lo32 = x | (g4 << 28) | (g5 << 3) | (g6 << 10) | (g7 << 17) | (g8 << 24) | (g9 << 31);
+    const bool neg = ((g4 >> 3) | g9) & 1u;
+    val = (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
+  } else {
+    val = (int64_t)((uint64_t)x | ((uint64_t)g4 << 28) | ((uint64_t)g5 << 35) | ((uint64_t)g6 << 42) |
+                    ((uint64_t)g7 << 49) | ((uint64_t)g8 << 56) | ((uint64_t)g9 << 63));
+  }
+  return true;
+}
+
+// A list holding exactly one value: the value itself, packed into the 8-byte loc word (int64 bits,
+// float bits in .x, or the bytes element's absolute (offset, length)). The gather then writes it
+// without touching the record again. false = keep the list location.
+template <bool COMPAT>
+__device__ __forceinline__ bool fast_single(const FastSrc& s, uint32_t kind, uint32_t lo, uint32_t ll, uint2& val) {
+  uint32_t q = lo, fn, co, cl;
+  if (!ffield(s, q, lo + ll, fn, co, cl) || fn != 1u || q != lo + ll) return false;
+  if (kind == TFRG_KIND_BYTES) {
+    val = make_uint2((uint32_t)(s.base + co), cl);
+    return true;
+  }
+  if (kind == TFRG_KIND_FLOAT) {
+    if (cl != 4u) return false;
+    val = make_uint2(lds_u32u(s.l, s.p + co), 0u);
+    return true;
+  }
+  // int64: one varint of <= 4 bytes filling the chunk (values < 2^28, same in both varint modes)
+  if (cl == 0u || cl > 4u) return false;
+  const uint32_t w = s.w4(co);
+  const uint32_t term = ~w & 0x80808080u;
+  if (!term || (__builtin_ctz(term) >> 3) + 1u != cl) return false;
+  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+  val = make_uint2(x & ((1u << (7u * cl)) - 1u), 0u);
+  return true;
+}
+
+template <bool COMPAT>
+__device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, CountSink& sink) {
   uint32_t pos = 0;
   const uint32_t L = s.L;
   bool have = false;
@@ -882,8 +953,11 @@ __device__ int fast_walk(const FastSrc& s, const LdsKeys& K, CountSink& sink) {
       if (sink.rank >= 65534u) return kBail;
       sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(++sink.rank);
       const size_t at = (size_t)slot * sink.n + sink.r;
-      sink.o->count[at] = cnt;
-      sink.o->loc[at] = make_uint2(lo, ll);
+      uint2 lv = make_uint2(lo, ll);
+      uint32_t cw = cnt;
+      if (cnt == 1u && fast_single<COMPAT>(s, kind, lo, ll, lv)) cw = 1u | kCountInline;
+      sink.o->count[at] = cw;
+      sink.o->loc[at] = lv;
     }
   }
   return have ? TFRG_OK : kBail;
@@ -935,7 +1009,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
   int status;
   if constexpr (STAGED) {
     const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-    status = fast_ok ? fast_walk(fs, K, sink) : kBail;
+    status = fast_ok ? fast_walk<COMPAT>(fs, K, sink) : kBail;
     if (status == kBail) {  // non-canonical record: exact reference walk from the same stage
       for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
       sink.rank = 0;
@@ -955,7 +1029,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
 // GORD: keep the per-record dict state in the global `order` column instead of LDS (key tables too
 // large for LDS); same results, slower.
 template <int R, bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kLaneBlock, 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1431,6 +1505,8 @@ __device__ __forceinline__ void load_items(const uint32_t* c, uint64_t base, uin
 #pragma unroll
     for (int i = 0; i < kScanItems; ++i) v[i] = base + i < n ? c[base + i] : 0u;
   }
+#pragma unroll
+  for (int i = 0; i < kScanItems; ++i) v[i] &= ~kCountInline;
 }
 
 // phase 1: per-tile sums -> tsum[slot][tile]
@@ -1551,46 +1627,6 @@ __device__ void list_gather(S& s, const DevOut& o, int kind, int64_t lo, int64_t
 // one int64 varint at `pos` of a validated packed chunk ending at `e` (fast path): <= 4 bytes from
 // one word, longer ones byte by byte with the reference's compat semantics; false = bail
 template <bool COMPAT>
-__device__ __forceinline__ bool fast_value(const FastSrc& s, uint32_t& pos, uint32_t e, int64_t& val) {
-  const uint32_t w = s.w4(pos);
-  const uint32_t term = ~w & 0x80808080u;
-  if (term) {
-    const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
-    if (pos + nb > e) return false;
-    const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-    val = (int64_t)(x & ((1u << (7u * nb)) - 1u));
-    pos += nb;
-    return true;
-  }
-  // 5..10 bytes: two more words, terminator found by bit scan, groups combined branch-free (no
-  // dependent byte-at-a-time chain: a long varint costs one extra LDS round trip)
-  const uint32_t w1 = s.w4s(pos + 4), w2 = s.w4s(pos + 8);
-  const uint32_t t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
-  uint32_t nb;
-  if (t1) nb = 5u + (__builtin_ctz(t1) >> 3);
-  else if (t2) nb = 9u + (__builtin_ctz(t2) >> 3);
-  else return false;  // > 10 bytes: "Too many bytes when decoding varint." (exact path)
-  if (pos + nb > e) return false;
-  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-  const uint32_t g4 = w1 & 0x7fu;
-  const uint32_t g5 = nb > 5u ? (w1 >> 8) & 0x7fu : 0u;
-  const uint32_t g6 = nb > 6u ? (w1 >> 16) & 0x7fu : 0u;
-  const uint32_t g7 = nb > 7u ? (w1 >> 24) & 0x7fu : 0u;
-  const uint32_t g8 = nb > 8u ? w2 & 0x7fu : 0u;
-  const uint32_t g9 = nb > 9u ? (w2 >> 8) & 0x7fu : 0u;
-  pos += nb;
-  if (COMPAT) {  // term_k = (int32)(g_k << (7k & 31)), sign-extended, OR-ed (decoder.pyx:34-50)
-    const uint32_t lo32 = x | (g4 << 28) | (g5 << 3) | (g6 << 10) | (g7 << 17) | (g8 << 24) | (g9 << 31);
-    const bool neg = ((g4 >> 3) | g9) & 1u;
-    val = (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
-  } else {
-    val = (int64_t)((uint64_t)x | ((uint64_t)g4 << 28) | ((uint64_t)g5 << 35) | ((uint64_t)g6 << 42) |
-                    ((uint64_t)g7 << 49) | ((uint64_t)g8 << 56) | ((uint64_t)g9 << 63));
-  }
-  return true;
-}
-
-template <bool COMPAT>
 __device__ __forceinline__ bool fast_list_gather(const FastSrc& s, const DevOut& o, uint32_t kind, uint32_t lo,
                                                  uint32_t ll, uint64_t dst) {
   uint32_t q = lo;
@@ -1624,15 +1660,30 @@ __device__ __forceinline__ bool fast_list_gather(const FastSrc& s, const DevOut&
   return true;
 }
 
+// values of every out-of-line present slot of record r (inline single values are written by the
+// caller's first pass)
 template <bool COMPAT, class S>
 __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t r,
                                               S& s) {
   for (uint32_t k = 0; k < sc.n_slots; ++k) {
     const size_t at = (size_t)k * B.n + r;
-    if (!o.order[at]) continue;
+    const uint32_t c = o.count[at];
+    if (!c || (c & kCountInline)) continue;
     const uint2 lc = o.loc[at];
     const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
     list_gather<COMPAT>(s, o, sc.slot_kind[k], (int64_t)lc.x, (int64_t)lc.y, dst);
+  }
+}
+
+// single value stored in the loc word by the count pass
+__device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2 lc, uint64_t dst) {
+  if (kind == TFRG_KIND_INT64) {
+    if (dst < o.cap_i64) o.i64[dst] = (int64_t)(((uint64_t)lc.y << 32) | lc.x);
+  } else if (kind == TFRG_KIND_FLOAT) {
+    if (dst < o.cap_f32) o.f32[dst] = lc.x;
+  } else if (dst < o.cap_b) {
+    o.b_off[dst] = lc.x;
+    o.b_len[dst] = lc.y;
   }
 }
 
@@ -1646,56 +1697,72 @@ __global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchem
        base += (uint64_t)gridDim.x * kLaneBlock) {
     const uint64_t ri = base + lane;
     const uint32_t r = (uint32_t)ri;
-    RecView v;
-    bool mine = false;
+    // pass 1: slot metadata (every load issued up front); inline single values written now. A
+    // non-zero count implies a decoded record with the slot present (failed records and absent
+    // slots have count 0), so neither status nor order is read.
+    bool need = false;
     if (ri < B.n) {
-      v = rec_view(B, r);
-      mine = v.status == TFRG_OK && v.e - v.st <= lane_max && o.status[r] == TFRG_OK;
-    }
-    uint64_t lo, hi;
-    wave_span(mine, v.st, v.e, lo, hi);
-    const uint64_t lo16 = lo & ~15ull;
-    const bool staged = hi > lo && hi - lo16 <= kStageBytes;
-    if (staged) {
-      stage_span(stage, B.bytes, lo16, hi, lane);
-      wave_lds_sync();
-    }
-    if (mine) {
-      if (staged) {
-        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-        LdsSrc s;
-        s.init(stage, lo16, v.p0, v.L);
-        for (uint32_t k0 = 0; k0 < sc.n_slots; k0 += 4) {
-          // issue every slot's metadata loads up front (no load waits on another)
-          uint32_t ordv[4], rsv[4];
-          uint2 lcv[4];
-          uint64_t basev[4];
+      for (uint32_t k0 = 0; k0 < sc.n_slots; k0 += 4) {
+        uint32_t cntv[4], rsv[4];
+        uint2 lcv[4];
+        uint64_t basev[4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t k = k0 + j < sc.n_slots ? k0 + j : k0;
-            const size_t at = (size_t)k * B.n + r;
-            ordv[j] = o.order[at];
-            lcv[j] = o.loc[at];
-            rsv[j] = o.rs[(size_t)k * (B.n + 1) + r];
-            basev[j] = o.slot_base[k];
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t k = k0 + j;
-            if (k >= sc.n_slots || !ordv[j]) continue;
-            const uint32_t kind = sc.slot_kind[k];
-            const uint64_t dst = basev[j] + rsv[j];
-            if (!fast_list_gather<COMPAT>(fs, o, kind, lcv[j].x, lcv[j].y, dst))
-              list_gather<COMPAT>(s, o, (int)kind, (int64_t)lcv[j].x, (int64_t)lcv[j].y, dst);
-          }
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t k = k0 + j < sc.n_slots ? k0 + j : k0;
+          const size_t at = (size_t)k * B.n + r;
+          cntv[j] = o.count[at];
+          lcv[j] = o.loc[at];
+          rsv[j] = o.rs[(size_t)k * (B.n + 1) + r];
+          basev[j] = o.slot_base[k];
         }
-      } else {
-        Src s;
-        s.init(B.bytes, v.p0, v.L);
-        gather_record<COMPAT>(B, sc, o, r, s);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const uint32_t k = k0 + j;
+          if (k >= sc.n_slots || !cntv[j]) continue;
+          if (cntv[j] & kCountInline) put_inline(o, sc.slot_kind[k], lcv[j], basev[j] + rsv[j]);
+          else need = true;
+        }
       }
     }
-    wave_lds_sync();
+    // pass 2 (only when some record of the wave has an out-of-line list): stage and decode;
+    // records above lane_max belong to the wavefront gather kernels
+    if (__ballot(need)) {
+      RecView v;
+      if (need) {
+        v = rec_view(B, r);
+        need = v.e - v.st <= lane_max;
+      }
+      uint64_t lo, hi;
+      wave_span(need, v.st, v.e, lo, hi);
+      const uint64_t lo16 = lo & ~15ull;
+      const bool staged = hi > lo && hi - lo16 <= kStageBytes;
+      if (staged) {
+        stage_span(stage, B.bytes, lo16, hi, lane);
+        wave_lds_sync();
+      }
+      if (need) {
+        if (staged) {
+          const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+          LdsSrc s;
+          s.init(stage, lo16, v.p0, v.L);
+          for (uint32_t k = 0; k < sc.n_slots; ++k) {
+            const size_t at = (size_t)k * B.n + r;
+            const uint32_t c = o.count[at];
+            if (!c || (c & kCountInline)) continue;
+            const uint2 lc = o.loc[at];
+            const uint32_t kind = sc.slot_kind[k];
+            const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+            if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
+              list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+          }
+        } else {
+          Src s;
+          s.init(B.bytes, v.p0, v.L);
+          gather_record<COMPAT>(B, sc, o, r, s);
+        }
+      }
+      wave_lds_sync();
+    }
   }
 }
 
