@@ -71,8 +71,9 @@ TFRG_HD inline uint32_t gf_xpow8_inv(uint64_t z) { return gf_pow(kXInverse, 8 * 
 
 // Byte table for slice-by-4 step tables: T[j][v] = U(0, v followed by j zero bytes)
 // (T[0] is the classic byte table).
+// (8 tables: slice-by-8; the first 4 are the slice-by-4 set)
 struct CrcTables {
-  uint32_t t[4][256];
+  uint32_t t[8][256];
 };
 
 inline void crc_make_tables(CrcTables* T) {
@@ -83,7 +84,7 @@ inline void crc_make_tables(CrcTables* T) {
   }
   for (uint32_t v = 0; v < 256; ++v) {
     uint32_t c = T->t[0][v];
-    for (int j = 1; j < 4; ++j) {
+    for (int j = 1; j < 8; ++j) {
       c = (c >> 8) ^ T->t[0][c & 0xff];
       T->t[j][v] = c;
     }

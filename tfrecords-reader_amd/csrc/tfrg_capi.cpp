@@ -105,15 +105,16 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
     set_error("hipStreamCreate failed");
     return TFRG_E_HIP;
   }
-  // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192; consts: 64 lane shifts x^(128 l)
-  // and 16 un-shifts x^(-8z)
-  std::vector<uint32_t> tab(2048), cst(80);
+  // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (wavefront kernels), then
+  // [8][256] slice-by-8 (lane kernel); consts: 64 lane shifts x^(128 l) and 16 un-shifts x^(-8z)
+  std::vector<uint32_t> tab(4096), cst(80);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
   uint32_t M[4][256];
   crc_make_mul_tables(gf_xpow8(1024), M);
   memcpy(tab.data() + 1024, M, 4096);
+  memcpy(tab.data() + 2048, T.t, 8192);
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||

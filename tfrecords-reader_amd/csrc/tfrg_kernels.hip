@@ -28,7 +28,7 @@ namespace tfrg {
 // Optional per-phase cycle accounting of the wavefront kernels (make prof -> libtfrg_prof.so);
 // compiled out of the product library.
 #ifdef TFRG_PHASE_PROF
-__device__ unsigned long long g_phase[16];
+__device__ unsigned long long g_phase[32];
 #define PHASE_MARK(t) const uint64_t t = __builtin_readcyclecounter()
 #define PHASE_ADD(i, a, b) \
   do {                     \
@@ -452,6 +452,12 @@ struct LdsTab {
   __device__ __forceinline__ uint32_t step1(uint32_t c_, uint32_t byte) const {
     return (*this)(0, (c_ ^ byte) & 0xffu) ^ (c_ >> 8);
   }
+  // 8 bytes (x = state ^ first word, y = second word); needs the slice-by-8 table set
+  __device__ __forceinline__ uint32_t step8(uint32_t x, uint32_t y) const {
+    return (*this)(7, x & 0xffu) ^ (*this)(6, (x >> 8) & 0xffu) ^ (*this)(5, (x >> 16) & 0xffu) ^
+           (*this)(4, x >> 24) ^ (*this)(3, y & 0xffu) ^ (*this)(2, (y >> 8) & 0xffu) ^
+           (*this)(1, (y >> 16) & 0xffu) ^ (*this)(0, y >> 24);
+  }
 };
 
 // Serial CRC-32C of absolute bytes [a, b) by one lane: aligned 16 B loads, slice-by-4 for whole
@@ -540,6 +546,7 @@ __device__ uint32_t crc_wave(const uint8_t* buf, uint64_t a, uint64_t b, const L
 // ------------------------------------------------------------------------------------------------
 struct RecView {
   uint64_t st, e;   // absolute [st, e) clamped to the buffer
+  uint64_t en;      // end as given (unclamped; the framing length check compares against it)
   uint64_t p0;
   int64_t L;
   int status;
@@ -549,6 +556,7 @@ struct RecView {
 __device__ __forceinline__ RecView rec_view_se(const DevBatch& B, uint64_t st, uint64_t en) {
   RecView v;
   v.st = st;
+  v.en = en;
   v.status = TFRG_OK;
   v.verdict = 0;
   const bool framed = !(B.flags & kFlagPayloadOnly);
@@ -693,6 +701,22 @@ __device__ uint32_t crc_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsT
   while (a < b && (a & 3u)) c = T.step1(c, l[a++]);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
   for (; a + 4 <= b; a += 4) c = T.step4(c ^ w[a >> 2]);
+  while (a < b) c = T.step1(c, l[a++]);
+  return ~c;
+}
+
+// as crc_lds, 8 bytes per dependent step (T holds the slice-by-8 set): half the table-lookup
+// chain of slice-by-4 for the lane kernel's short records
+template <int R>
+__device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<R>& T) {
+  uint32_t c = 0xffffffffu;
+  while (a < b && (a & 3u)) c = T.step1(c, l[a++]);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
+  for (; a + 8 <= b; a += 8) c = T.step8(c ^ w[a >> 2], w[(a >> 2) + 1]);
+  if (a + 4 <= b) {
+    c = T.step4(c ^ w[a >> 2]);
+    a += 4;
+  }
   while (a < b) c = T.step1(c, l[a++]);
   return ~c;
 }
@@ -970,6 +994,10 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
                                          const LdsKeys& K, bool fast_ok, int64_t& aux) {
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
+#ifdef TFRG_PHASE_PROF
+  const uint32_t lane = threadIdx.x & 63u;
+#endif
+  PHASE_MARK(c0);
   if (framed) {
     const uint64_t D = v.e - v.st;
     if (D >= 8) {
@@ -980,11 +1008,11 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
       } else {
         lenf = load_u64_unaligned(B.bytes, v.st);
       }
-      if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+      if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
       if (do_crc && D >= 12) {
         uint32_t c, stored;
         if constexpr (STAGED) {
-          c = crc_lds<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
+          c = crc_lds8<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
           stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
         } else {
           c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
@@ -995,7 +1023,7 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
       if (do_crc && D >= 16) {
         uint32_t c, stored;
         if constexpr (STAGED) {
-          c = crc_lds<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+          c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
           stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
         } else {
           c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
@@ -1005,6 +1033,8 @@ __device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc,
       }
     }
   }
+  PHASE_MARK(c1);
+  PHASE_ADD(17, c0, c1);
   for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
   int status;
   if constexpr (STAGED) {
@@ -1033,17 +1063,17 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
                                                            const uint32_t* __restrict__ crc_tab,
                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;                                           // 1024 * R dwords
-  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 1024 * R);   // [n_slots][kLaneBlock]
+  uint32_t* tab = lds;                                           // 2048 * R dwords (slice-by-8)
+  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 2048 * R);   // [n_slots][kLaneBlock]
   const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * kLaneBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage_all = reinterpret_cast<uint8_t*>(lds + 1024 * R) + ord_bytes;
+  uint8_t* stage_all = reinterpret_cast<uint8_t*>(lds + 2048 * R) + ord_bytes;
   uint8_t* stage = stage_all + wib * kStageStride;
   // key table for the fast path (after the 4 wave stages)
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
   uint32_t* krec = kht + kLdsMaxHt;
-  for (uint32_t i = threadIdx.x; i < 1024u * R; i += kLaneBlock) tab[i] = crc_tab[i / R];
+  for (uint32_t i = threadIdx.x; i < 2048u * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
@@ -1054,6 +1084,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
 
   for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
        base += (uint64_t)gridDim.x * kLaneBlock) {
+    PHASE_MARK(t0);
     const uint64_t ri = base + lane;
     const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
@@ -1083,6 +1114,8 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
+    PHASE_MARK(t1);
+    PHASE_ADD(16, t0, t1);
     if (mine) {
       int64_t aux = 0;
       CountSink sink{&sc, &o, GORD ? o.order + r : ord + threadIdx.x, GORD ? B.n : (uint32_t)kLaneBlock, 0,
@@ -1092,10 +1125,16 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
         status = staged ? count_one<R, COMPAT, true>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux)
                         : count_one<R, COMPAT, false>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux);
       }
+      PHASE_MARK(t3);
       sink.finalize(status == TFRG_OK);
       record_result(o, r, status, aux, v.verdict);
+      PHASE_MARK(t4);
+      PHASE_ADD(19, t3, t4);
     }
     wave_lds_sync();  // the stage is rewritten by the next iteration
+    PHASE_MARK(t2);
+    PHASE_ADD(20, t0, t2);
+    PHASE_ADD(18, t1, t2);
   }
 }
 
@@ -1228,7 +1267,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
       const uint64_t D = v.e - v.st;
       if (D >= 8) {
         const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
-        if (lenf == B.end[r] - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+        if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
         if (do_crc && D >= 12) {
           const uint32_t c = crc_serial<1>(B.bytes, v.st, v.st + 8, T);
           if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
@@ -1909,7 +1948,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
 // ------------------------------------------------------------------------------------------------
 // launcher
 // ------------------------------------------------------------------------------------------------
-constexpr int kLaneRep = 4;  // CRC table bank replication in the lane kernel
+constexpr int kLaneRep = 2;  // CRC table bank replication in the lane kernel (slice-by-8: 16 KiB)
 
 constexpr size_t kLdsBudget = 128 * 1024;  // above this the dict state goes to the global column
 
@@ -1922,7 +1961,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   auto mark = [&](int i) {
     if (ev) (void)hipEventRecord(ev[i], st);
   };
-  const size_t tab_lds = 1024ull * kLaneRep * 4;
+  const size_t tab_lds = 2048ull * kLaneRep * 4;
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
   const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
                               ? (kLdsMaxHt + (size_t)sc.n_keys * kKrWords) * 4 : 0;
@@ -2021,10 +2060,10 @@ hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hi
 
 #ifdef TFRG_PHASE_PROF
 extern "C" int tfrg_debug_phase(unsigned long long* out, int n, int reset) {
-  if (n > 16) n = 16;
+  if (n > 32) n = 32;
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(tfrg::g_phase), n * sizeof(unsigned long long)) != hipSuccess) return -2;
   if (reset) {
-    unsigned long long z[16] = {};
+    unsigned long long z[32] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(tfrg::g_phase), z, sizeof(z)) != hipSuccess) return -2;
   }
   return n;

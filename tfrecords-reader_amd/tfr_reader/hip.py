@@ -264,6 +264,7 @@ class BatchResult:
     bytes_len: np.ndarray
     slot_key: list[str]
     slot_kind: list[int]
+    _lay = None  # (record -> layout index, layouts), built on first use
 
     def __len__(self) -> int:
         return int(self.status.shape[0])
@@ -310,15 +311,120 @@ class BatchResult:
         return {self.slot_key[s]: ColumnFeature(self, int(s), i) for s in present.tolist()}
 
     def feature(self, i: int):
+        """Record i as a ``Feature`` (raises the record's exception)."""
         from tfr_reader.example.feature import Feature  # noqa: PLC0415
 
-        return Feature(self.record_dict(i))
+        self.raise_for(i)
+        if self._lay is None:
+            self._lay = self._layouts()
+        inv, layouts = self._lay
+        return Feature(_RecordView(self, i, layouts[int(inv[i])]))
 
-    def features(self) -> list:
-        return [self.feature(i) for i in range(len(self))]
+    def _layouts(self) -> tuple[np.ndarray, list[_Layout]]:
+        """Per record, the index of its key layout (present slots in dict order); records of a
+        dataset share a handful of layouts, so the per-record work is one array lookup."""
+        ns, n = self.order.shape
+        if ns == 0:
+            return np.zeros(n, np.int64), [_Layout((), self.slot_key)]
+        if ns <= 4:
+            sig = np.zeros(n, np.uint64)
+            for s in range(ns):
+                sig |= self.order[s].astype(np.uint64) << np.uint64(16 * s)
+            uniq, inv = np.unique(sig, return_inverse=True)
+            cols = [[(int(u) >> (16 * s)) & 0xFFFF for s in range(ns)] for u in uniq.tolist()]
+        else:
+            uniq, inv = np.unique(np.ascontiguousarray(self.order.T), axis=0, return_inverse=True)
+            cols = uniq.tolist()
+        layouts = []
+        for col in cols:
+            present = sorted((rk, s) for s, rk in enumerate(col) if rk)
+            layouts.append(_Layout(tuple(s for _, s in present), self.slot_key))
+        return inv.reshape(-1), layouts
+
+    def features(self, start: int = 0, stop: int | None = None) -> list:
+        """Records [start, stop) as ``Feature`` objects (lazy column views). Raises the first
+        failing record's exception, in record order, like decoding them one by one."""
+        from tfr_reader.example.feature import Feature  # noqa: PLC0415
+
+        stop = len(self) if stop is None else min(stop, len(self))
+        bad = np.flatnonzero(self.status[start:stop])
+        if bad.size:
+            self.raise_for(start + int(bad[0]))
+        if self._lay is None:
+            self._lay = self._layouts()
+        inv, layouts = self._lay
+        return [Feature(_RecordView(self, i, layouts[j]))
+                for i, j in zip(range(start, stop), inv[start:stop].tolist())]
+
+    def column(self, key: str, kind: str | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """Ragged column of one key over the batch: (values, offsets) with record i's values at
+        ``values[offsets[i]:offsets[i + 1]]`` (numpy views of the fetched columns; floats as
+        float32, bytes as an object array of ``bytes``). Records without the key contribute none."""
+        slots = [s for s, k in enumerate(self.slot_key) if k == key and (kind is None or
+                                                                      KIND_NAMES[self.slot_kind[s]] == kind)]
+        if not slots:
+            raise KeyError(key)
+        if len(slots) > 1:
+            raise ValueError(f"key {key!r} has several kinds in this batch; pass kind=")
+        s = slots[0]
+        base = int(self.slot_base[s])
+        rs = self.row_splits[s].astype(np.int64)
+        lo, hi = base + int(rs[0]), base + int(rs[-1])
+        k = self.slot_kind[s]
+        if k == 3:
+            vals = self.i64[lo:hi]
+        elif k == 2:
+            vals = self.f32[lo:hi].view(np.float32)
+        else:
+            b = self.buf
+            vals = np.array([b[o : o + ln].tobytes() for o, ln in
+                             zip(self.bytes_off[lo:hi].tolist(), self.bytes_len[lo:hi].tolist())], dtype=object)
+        return vals, rs - rs[0]
 
     def crc_ok(self) -> np.ndarray:
         return (self.verdict & 6) == 6
+
+
+class _Layout:
+    """Present slots of a record in dict order, with the key -> slot map they imply."""
+
+    __slots__ = ("slots", "keys", "index")
+
+    def __init__(self, slots: tuple[int, ...], slot_key: list[str]) -> None:
+        self.slots = slots
+        self.keys = [slot_key[s] for s in slots]
+        self.index = dict(zip(self.keys, slots))
+
+
+class _RecordView:
+    """Read-only ``key -> ColumnFeature`` mapping of one record (what ``Feature`` wraps); the
+    column views are built on access."""
+
+    __slots__ = ("_r", "_i", "_l")
+
+    def __init__(self, r: BatchResult, i: int, layout: _Layout) -> None:
+        self._r, self._i, self._l = r, i, layout
+
+    def __len__(self) -> int:
+        return len(self._l.slots)
+
+    def __iter__(self):
+        return iter(self._l.keys)
+
+    def __contains__(self, key) -> bool:
+        return key in self._l.index
+
+    def keys(self):
+        return list(self._l.keys)
+
+    def __getitem__(self, key: str) -> ColumnFeature:
+        return ColumnFeature(self._r, self._l.index[key], self._i)
+
+    def items(self):
+        return [(k, ColumnFeature(self._r, s, self._i)) for k, s in zip(self._l.keys, self._l.slots)]
+
+    def values(self):
+        return [ColumnFeature(self._r, s, self._i) for s in self._l.slots]
 
 
 class _ValueList:
