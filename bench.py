@@ -142,7 +142,9 @@ def main() -> None:
     d_st = torch.from_numpy(st.view(np.int64)).to(dev)
     d_en = torch.from_numpy(en.view(np.int64)).to(dev)
     del big
-    stream = torch.cuda.current_stream(dev)
+    # a dedicated stream: torch's default stream has handle 0, which the C-ABI reads as "use the
+    # context's own stream", and events recorded on it would not bracket the decode
+    stream = torch.cuda.Stream(dev)
 
     dec = hip.HipDecoder(local)
     dec.decode(*sample)  # learns the key table (host path, schema-miss rounds)

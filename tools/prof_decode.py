@@ -55,7 +55,7 @@ def main():
 
         (ctypes.c_ulonglong * 16)()
         _native.lib().tfrg_debug_phase((ctypes.c_ulonglong * 16)(), 16, 1)
-    s = torch.cuda.current_stream(dev)
+    s = torch.cuda.Stream(dev)
     dec.set_profiling(True)
     for _ in range(a.iters):
         dec.decode_device(d_b.data_ptr(), big.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0], stream=s.cuda_stream,
