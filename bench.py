@@ -147,7 +147,8 @@ def main() -> None:
     stream = torch.cuda.Stream(dev)
 
     dec = hip.HipDecoder(local)
-    dec.decode(*sample)  # learns the key table (host path, schema-miss rounds)
+    res0 = dec.decode(*sample)  # learns the key table (host path, schema-miss rounds)
+    present_per_rec = float((res0.order != 0).sum()) / max(1, int(sample[1].shape[0]))
 
     def step():
         dec.decode_device(d_bytes.data_ptr(), nbytes, d_st.data_ptr(), d_en.data_ptr(), n, stream=stream.cuda_stream)
@@ -195,24 +196,31 @@ def main() -> None:
     kern_ms = {k: float(np.mean(v)) for k, v in per.items()}
     dominant = max(kern_ms, key=kern_ms.get)
 
-    # algorithmic bytes per launch. Count kernels (lane / wave) read every
-    # framed byte of their records plus the two u64 offsets and write the u32 status; gather
-    # kernels write the values (8 B int64, 4 B float, 8 B bytes view) and one u32 row split per
-    # (slot, record).
+    # algorithmic bytes per launch: the compulsory HBM traffic of each kernel.
+    # Lane count: every framed byte of its records + the two u64 offsets, status (4 B) + verdict
+    # (1 B) + order/count (2 + 4 B per slot) + one loc word (8 B) per present list. Wave count: the
+    # framed bytes + offsets. Down-gather: counts read, row splits written (4 + 4 B per slot and
+    # record), every value written (8 B int64 / 4 B float / 8 B bytes view) and the loc word it comes
+    # from when inline. Spine: tile sums read + written.
     n_slots = len(dec.keys.slot_key)
     n_big = int(info.n_big)
-    big_bytes = 0
-    if n_big:
-        sz = (en - st)
-        big_bytes = int(sz[sz > hip.DEFAULT_LANE_MAX].sum())
+    sz = en - st
+    big_sel = sz > hip.DEFAULT_LANE_MAX
+    big_bytes = int(sz[big_sel].sum())
     small_bytes = framed_bytes - big_bytes
+    n_small = n - n_big
+    present_small = int(present_per_rec * n_small)
+    n_vals = int(info.kind_totals[3]) + int(info.kind_totals[2]) + int(info.kind_totals[1])
     vals = 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 8 * int(info.kind_totals[1])
+    n_tiles = (n + 255) // 256
     alg = {
-        "k_lane_count": small_bytes + 20 * (n - n_big),
-        "k_wave_count": big_bytes + 20 * n_big,
-        "k_lane_gather": vals + 4 * n * n_slots,
-        "k_wave_gather": vals + 4 * n * n_slots,
-        "k_scan": 12 * n * n_slots,
+        "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
+        "k_slow_count": 0,
+        "k_wave_count": big_bytes + 16 * n_big,
+        "k_spine": 8 * n_slots * n_tiles,
+        "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
+        "k_list_gather": vals,
+        "k_wave_gather": vals,
     }
     a_bytes = alg.get(dominant, framed_bytes + 20 * n)
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9

@@ -136,6 +136,32 @@ def test_c1_shape_vs_oracle(dec, orc):
     assert np.array_equal(labels, np.arange(65536) % 1000)
 
 
+def test_lane_crc_verdicts_every_alignment(dec, orc):
+    """Lane-path CRC-32C over every payload length 9..200 and start alignment, with flipped bits in
+    the length CRC, the payload and the data CRC of some records: verdicts, status and values vs
+    the oracle record by record."""
+    from tests.golden.gen_golden import byt, entry, example, i64
+
+    pl = []
+    for i in range(800):
+        m = i % 190
+        pl.append(example(entry(b"k", byt(bytes([i & 0xFF]) * m)), entry(b"n", i64(*range(i % 5)))))
+    buf, st, en = synth.framed(pl, crc=True)
+    b = buf.copy()
+    for i in range(len(pl)):
+        s, e = int(st[i]), int(en[i])
+        if i % 7 == 1:
+            b[s + 8 + i % 4] ^= 0x10  # length CRC
+        elif i % 7 == 2:
+            b[s + 12 + (i * 13) % (e - s - 16)] ^= 0x01  # payload (may also break the decode)
+        elif i % 7 == 3:
+            b[e - 4 + i % 4] ^= 0x80  # data CRC
+    r = dec.decode(b, st, en)
+    assert r.info.n_big == 0
+    bad = _compare_to_oracle(r, orc, b, st, en)
+    assert not bad, bad[:10]
+
+
 def test_c2_shape_vs_oracle(dec, orc):
     """Large skewed records (wavefront kernels: wave CRC, bytes views)."""
     buf, st, en = synth.framed(synth.c2_payloads(96, seed=5))

@@ -73,7 +73,7 @@ struct tfrg_ctx {
   DBuf in_bytes, in_start, in_end;
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
-  DBuf i64, f32, b_off, b_len, big_list, miss, info, tsum;
+  DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum;
   // last batch
   uint32_t n = 0;
   uint64_t nbytes = 0;
@@ -135,7 +135,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
-                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->miss, &c->info, &c->tsum};
+                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum};
   for (DBuf* b : all) b->release();
   if (c->have_events)
     for (auto& e : c->ev) (void)hipEventDestroy(e);
@@ -282,29 +282,32 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
   const uint32_t S = c->n_slots;
   const uint64_t nn = n ? n : 1;
-  const uint32_t n_tiles = (n + kScanTile - 1) / kScanTile;
+  const uint32_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
+  const uint32_t tile_stride = (n_tiles + 3u) & ~3u;
   const uint64_t cap_i64 = nbytes + 16, cap_f32 = nbytes / 4 + 16, cap_b = nbytes / 2 + 16;
   // growing an arena buffer frees the old one: wait for work that may still read it
   bool grow = c->status.cap < nn * 4 || c->aux.cap < nn * 8 || c->verdict.cap < nn ||
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
               c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
-              c->tsum.cap < (uint64_t)S * n_tiles * 4 + 8;
+              c->slow_list.cap < nn * 4 || c->tsum.cap < (uint64_t)S * tile_stride * 4 + 16;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
       c->count.ensure(S * nn * 4) || c->loc.ensure(S * nn * 8) || c->rs.ensure(S * (nn + 1) * 4) ||
       c->slot_base.ensure((S + 1) * 8) || c->totals.ensure((S + 1) * 4) || c->kind_totals.ensure(32) ||
       c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
-      c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->miss.ensure(kMissCap * 16ull) ||
-      c->info.ensure(kInfoCount * 4) || c->tsum.ensure((uint64_t)S * n_tiles * 4 + 8)) {
+      c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->slow_list.ensure(nn * 4) ||
+      c->miss.ensure(kMissCap * 16ull) || c->info.ensure(kInfoCount * 4) ||
+      c->tsum.ensure((uint64_t)S * tile_stride * 4 + 16)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
   // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
   HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
   HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
-  if (S) HIP_TRY(hipMemsetAsync(c->totals.p, 0, S * 4, st));
+  if (S && n) HIP_TRY(hipMemsetAsync(c->tsum.p, 0, (size_t)S * tile_stride * 4, st));
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
+  if (!S || !n) HIP_TRY(hipMemsetAsync(c->kind_totals.p, 0, 32, st));
 
   DevBatch b;
   b.bytes = d_bytes;
@@ -336,7 +339,10 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.miss_cap = kMissCap;
   o.info = c->info.as<uint32_t>();
   o.tsum = c->tsum.as<uint32_t>();
+  o.tile_stride = tile_stride;
+  o.slow_list = c->slow_list.as<uint32_t>();
   LaunchCfg cfg;
+  cfg.num_cus = c->num_cus;
   const uint64_t lane_blocks = (n + 255) / 256;
   const uint64_t lane_cap = (uint64_t)c->num_cus * 8;
   cfg.lane_grid = (int)(lane_blocks < 1 ? 1 : (lane_blocks < lane_cap ? lane_blocks : lane_cap));
@@ -359,8 +365,6 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       set_error(std::string("kernel launch: ") + hipGetErrorString(e));
       return TFRG_E_HIP;
     }
-  } else {
-    HIP_TRY(hipMemsetAsync(c->kind_totals.p, 0, 32, st));
   }
   c->n = n;
   c->nbytes = nbytes;

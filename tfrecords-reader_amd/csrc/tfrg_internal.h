@@ -56,6 +56,9 @@ enum InfoIdx : uint32_t {
   kInfoBig = 4,          // records routed to the wave-per-record kernels
   kInfoScanTimeout = 5,  // reserved (always 0: the scan has no inter-workgroup waits)
   kInfoHuge = 6,         // wave records too large for the LDS stage (listed from the end of big_list)
+  kInfoSlow = 7,         // lane records left to the exact (slow) walker
+  kInfoSpineDone = 8,    // spine workgroups finished (the last one computes the column bases)
+  kInfoNeed = 9,         // lane records with an out-of-line list (k_list_gather; listed in slow_list)
   kInfoCount = 16
 };
 
@@ -82,29 +85,34 @@ struct DevOut {
   uint32_t* miss;        // [miss_cap][4] (record, kind, key abs offset, key length)
   uint32_t miss_cap;
   uint32_t* info;        // [kInfoCount]
-  uint32_t* tsum;        // [n_slots][n_tiles] scan tile sums / prefixes
+  uint32_t* tsum;        // [n_slots][tile_stride] per-tile value counts, then their exclusive prefixes
+  uint32_t tile_stride;  // >= n_tiles, multiple of 4
+  uint32_t* slow_list;   // [n] lane records for the exact walker; reused by k_down_gather for the
+                         // records k_list_gather decodes (the slow list is consumed by then)
 };
+
+// Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)
+constexpr uint32_t kTileShift = 8;
+constexpr uint32_t kTileRecs = 1u << kTileShift;
 
 // flags (mirrors include/tfrg.h)
 constexpr uint32_t kFlagPayloadOnly = 1u;
 constexpr uint32_t kFlagSpecVarint = 2u;
 constexpr uint32_t kFlagNoCrc = 4u;
 
-constexpr int kScanBlock = 256;
-constexpr int kScanItems = 16;
-constexpr uint32_t kScanTile = kScanBlock * kScanItems;
 
 // launchers (tfrg_kernels.hip)
 struct LaunchCfg {
-  int lane_grid;
+  int num_cus;
+  int lane_grid;           // cap: workgroups for one record per lane
   int wave_grid;
   uint32_t lane_max;       // records above this size go to the wave kernels
   uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageWaveCount, kStageScan, kStageBase, kStageLaneGather, kStageWaveGather,
-                   kNumStages };
+enum Stage : int { kStageLaneCount = 0, kStageSlowCount, kStageWaveCount, kStageSpine, kStageDownGather,
+                   kStageListGather, kStageWaveGather, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

@@ -19,6 +19,7 @@
 //
 // All walks share one templated walker so the lane and wave paths cannot drift apart.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include "tfrg_internal.h"
 #include "crc32c.h"
 #include "../../include/tfrg_status.h"
@@ -335,16 +336,26 @@ __device__ int walk_example(S& s, Sink& sink, int64_t& aux) {
 // Count sink: dict semantics (insertion order, last value wins, first position kept) over
 // (key, kind) slots, with the per-record rank state in LDS.
 // ------------------------------------------------------------------------------------------------
-struct CountSink {
+// L: the dict lives in LDS (ord + cnt, explicitly LDS-typed so every access is a ds_* instruction,
+// never a flat one); !L: in the global order / count columns (key tables too large for LDS).
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+
+template <bool L>
+struct CountSinkT {
+  using ord_t = std::conditional_t<L, lds_u16, uint16_t>;
+  using cnt_t = std::conditional_t<L, lds_u32, uint32_t>;
+  static constexpr bool kLds = L;
   const DevSchema* sc;
   const DevOut* o;
-  uint16_t* ord;     // LDS, ord[slot * ostride]
+  ord_t* ord;        // ord[slot * ostride]
   uint32_t ostride;
   uint32_t rank;
   uint32_t n, r;
   uint64_t p0;
   bool miss;
   bool leader;       // issues global writes and atomics
+  cnt_t* cnt = nullptr;  // LDS value counts, same layout as ord (L only)
 
   __device__ __forceinline__ void reset() {
     for (uint32_t k = 0; k < sc->n_slots; ++k) ord[(size_t)k * ostride] = 0;
@@ -416,25 +427,42 @@ struct CountSink {
     }
     ord[(size_t)slot * ostride] = (uint16_t)rk;
     if (count & kCountInline) return TFRG_ST_LIMIT;  // >= 2^31 values in one list
+    if constexpr (L) cnt[(size_t)slot * ostride] = count;
     if (leader) {
       const size_t at = (size_t)slot * n + r;
-      o->count[at] = count;
+      if constexpr (!L) o->count[at] = count;
       o->loc[at] = make_uint2((uint32_t)lo, (uint32_t)ll);
     }
     return TFRG_OK;
   }
 
+  // final count of a present slot (LDS, or read back from this thread's own column write)
+  __device__ __forceinline__ uint32_t count_of(uint32_t k) const {
+    if constexpr (L) return cnt[(size_t)k * ostride];
+    else return o->count[(size_t)k * n + r];
+  }
+
+  // dict -> order / count columns of a lane-per-record walk; present counts are added to the
+  // record's tile sum (the row-split scan's first level)
   __device__ __forceinline__ void finalize(bool ok) {
     for (uint32_t k = 0; k < sc->n_slots; ++k) {
       const uint32_t v = ok ? ord[(size_t)k * ostride] : 0u;
+      const uint32_t c = v ? count_of(k) : 0u;
       if (leader) {
         const size_t at = (size_t)k * n + r;
         o->order[at] = (uint16_t)v;
-        if (!v) o->count[at] = 0;
+        o->count[at] = c;
+        if (c & ~kCountInline) atomicAdd(&o->tsum[(size_t)k * o->tile_stride + (r >> kTileShift)], c & ~kCountInline);
       }
     }
   }
 };
+
+template <bool L>
+__device__ __forceinline__ typename CountSinkT<L>::ord_t* dict_ord(uint16_t* global, uint16_t* shared) {
+  if constexpr (L) return (lds_u16*)shared;
+  else return global;
+}
 
 // ------------------------------------------------------------------------------------------------
 // CRC-32C helpers
@@ -689,9 +717,9 @@ __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uin
 // 4 unaligned bytes at stage offset `off` (two aligned LDS dwords + a byte funnel shift)
 __device__ __forceinline__ uint32_t lds_u32u(const uint8_t* l, uint32_t off) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
-  const uint32_t a = off >> 2, sh = off & 3u;
-  const uint32_t lo = w[a];
-  return sh ? __builtin_amdgcn_alignbyte(w[a + 1], lo, sh) : lo;  // shift in bytes
+  const uint32_t a = off >> 2;
+  // always both dwords (one ds_read2_b32, no divergent branch); alignbyte by 0 returns the low one
+  return __builtin_amdgcn_alignbyte(w[a + 1], w[a], off & 3u);
 }
 
 // CRC-32C of stage bytes [a, b): byte steps to 4-alignment, slice-by-4 words, byte tail
@@ -705,19 +733,39 @@ __device__ uint32_t crc_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsT
   return ~c;
 }
 
-// as crc_lds, 8 bytes per dependent step (T holds the slice-by-8 set): half the table-lookup
-// chain of slice-by-4 for the lane kernel's short records
+// as crc_lds, 8 bytes per dependent step (T holds the slice-by-8 set), with no byte loops: the
+// k = a & 3 bytes before `a` in its dword are read as zeros and the start state is ~0 (x) x^(-8k)
+// (prepending zero bytes to a message multiplies the state by x^8 each, crc32c.h), and the last
+// m = b & 3 bytes take one partial slicing step T[m-1][x0] ^ ... ^ T[0][x(m-1)] ^ (c >> 8m).
+__device__ __forceinline__ uint32_t crc_head_state(uint32_t k) {
+  // ~0 (x) x^(-8k) for k = 0..3 (checked against crc32c("123456789") with k zero bytes prepended)
+  return k == 0 ? 0xffffffffu : (k == 1 ? 0xa942e6bcu : (k == 2 ? 0x2804363bu : 0x96db52a8u));
+}
 template <int R>
 __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<R>& T) {
-  uint32_t c = 0xffffffffu;
-  while (a < b && (a & 3u)) c = T.step1(c, l[a++]);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
-  for (; a + 8 <= b; a += 8) c = T.step8(c ^ w[a >> 2], w[(a >> 2) + 1]);
-  if (a + 4 <= b) {
-    c = T.step4(c ^ w[a >> 2]);
-    a += 4;
+  const uint32_t k = a & 3u, bw = b & ~3u, m = b & 3u;
+  uint32_t p = a & ~3u;
+  uint32_t c = crc_head_state(k);
+  uint32_t hm = 0xffffffffu << (8u * k);  // masks the bytes before a in the first dword
+  for (; p + 8 <= bw; p += 8) {
+    c = T.step8(c ^ (w[p >> 2] & hm), w[(p >> 2) + 1]);
+    hm = 0xffffffffu;
   }
-  while (a < b) c = T.step1(c, l[a++]);
+  if (p + 4 <= bw) {
+    c = T.step4(c ^ (w[p >> 2] & hm));
+    hm = 0xffffffffu;
+    p += 4;
+  }
+  if (m) {  // partial dword: m = 1..3 bytes
+    const uint32_t x = c ^ (w[p >> 2] & hm);
+    uint32_t t = T(m - 1u, x & 0xffu);
+    const uint32_t t1 = T(m >= 2u ? m - 2u : 0u, (x >> 8) & 0xffu);
+    const uint32_t t2 = T(0u, (x >> 16) & 0xffu);
+    t ^= m >= 2u ? t1 : 0u;
+    t ^= m == 3u ? t2 : 0u;
+    c = t ^ (c >> (8u * m));
+  }
   return ~c;
 }
 
@@ -936,8 +984,8 @@ __device__ __forceinline__ bool fast_single(const FastSrc& s, uint32_t kind, uin
   return true;
 }
 
-template <bool COMPAT>
-__device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, CountSink& sink) {
+template <bool COMPAT, class Sink>
+__device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Sink& sink) {
   uint32_t pos = 0;
   const uint32_t L = s.L;
   bool have = false;
@@ -980,100 +1028,87 @@ __device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Cou
       uint2 lv = make_uint2(lo, ll);
       uint32_t cw = cnt;
       if (cnt == 1u && fast_single<COMPAT>(s, kind, lo, ll, lv)) cw = 1u | kCountInline;
-      sink.o->count[at] = cw;
+      if constexpr (Sink::kLds) sink.cnt[(size_t)slot * sink.ostride] = cw;
+      else sink.o->count[at] = cw;
       sink.o->loc[at] = lv;
     }
   }
   return have ? TFRG_OK : kBail;
 }
 
-// Framing verdicts + reference walk of one record (lane-per-record), from the stage or from HBM.
-template <int R, bool COMPAT, bool STAGED>
-__device__ __forceinline__ int count_one(const DevBatch& B, const DevSchema& sc, uint32_t r, RecView& v,
-                                         CountSink& sink, const LdsTab<R>& T, const uint8_t* stage, uint64_t lo16,
-                                         const LdsKeys& K, bool fast_ok, int64_t& aux) {
-  const bool framed = !(B.flags & kFlagPayloadOnly);
-  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-#ifdef TFRG_PHASE_PROF
-  const uint32_t lane = threadIdx.x & 63u;
-#endif
-  PHASE_MARK(c0);
-  if (framed) {
-    const uint64_t D = v.e - v.st;
-    if (D >= 8) {
-      uint64_t lenf;
-      if constexpr (STAGED) {
-        const uint32_t o0 = (uint32_t)(v.st - lo16);
-        lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
-      } else {
-        lenf = load_u64_unaligned(B.bytes, v.st);
-      }
-      if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
-      if (do_crc && D >= 12) {
-        uint32_t c, stored;
-        if constexpr (STAGED) {
-          c = crc_lds8<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
-          stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
-        } else {
-          c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
-          stored = load_u32_unaligned(B.bytes, v.st + 8);
-        }
-        if (crc_mask(c) == stored) v.verdict |= TFRG_V_LEN_CRC;
-      }
-      if (do_crc && D >= 16) {
-        uint32_t c, stored;
-        if constexpr (STAGED) {
-          c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
-          stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
-        } else {
-          c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
-          stored = load_u32_unaligned(B.bytes, v.e - 4);
-        }
-        if (crc_mask(c) == stored) v.verdict |= TFRG_V_DATA_CRC;
-      }
-    }
-  }
-  PHASE_MARK(c1);
-  PHASE_ADD(17, c0, c1);
-  for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
-  int status;
+// Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
+// bytes and of the payload (the TFRecord spec; absent from the reference), from the
+// wave's LDS stage (STAGED) or from HBM.
+template <int R, bool STAGED>
+__device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, const LdsTab<R>& T, const uint8_t* stage,
+                                               uint64_t lo16) {
+  if (B.flags & kFlagPayloadOnly) return;
+  const bool do_crc = !(B.flags & kFlagNoCrc);
+  const uint64_t D = v.e - v.st;
+  if (D < 8) return;
+  uint64_t lenf;
   if constexpr (STAGED) {
-    const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-    status = fast_ok ? fast_walk<COMPAT>(fs, K, sink) : kBail;
-    if (status == kBail) {  // non-canonical record: exact reference walk from the same stage
-      for (uint32_t k = 0; k < sc.n_slots; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
-      sink.rank = 0;
-      LdsSrc s;
-      s.init(stage, lo16, v.p0, v.L);
-      status = walk_example<COMPAT>(s, sink, aux);
-    }
+    const uint32_t o0 = (uint32_t)(v.st - lo16);
+    lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
   } else {
-    Src s;
-    s.init(B.bytes, v.p0, v.L);
-    status = walk_example<COMPAT>(s, sink, aux);
+    lenf = load_u64_unaligned(B.bytes, v.st);
   }
-  if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-  return status;
+  if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+  if (do_crc && D >= 12) {
+    uint32_t c, stored;
+    if constexpr (STAGED) {
+      c = crc_lds8<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
+      stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
+    } else {
+      c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
+      stored = load_u32_unaligned(B.bytes, v.st + 8);
+    }
+    if (crc_mask(c) == stored) v.verdict |= TFRG_V_LEN_CRC;
+  }
+  if (do_crc && D >= 16) {
+    uint32_t c, stored;
+    if constexpr (STAGED) {
+      c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+      stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
+    } else {
+      c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
+      stored = load_u32_unaligned(B.bytes, v.e - 4);
+    }
+    if (crc_mask(c) == stored) v.verdict |= TFRG_V_DATA_CRC;
+  }
 }
 
-// GORD: keep the per-record dict state in the global `order` column instead of LDS (key tables too
-// large for LDS); same results, slower.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
+  return x;
+}
+
+// Lane-per-record FAST path. Each wave copies the contiguous span of its 64 records into its LDS
+// stage, then every lane checks its record's framing + CRC and runs the single-pass canonical walker
+// (fast_walk). Records the fast walker does not accept (non-canonical, erroneous, unknown keys), records
+// of a wave whose span does not fit the stage and framing errors are listed for k_slow_count; records
+// above lane_max for the wavefront kernels. The per-slot value counts of the accepted records are
+// summed per 256-record tile (first level of the row-split scan).
+// GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
 template <int R, bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab,
-                                                           uint32_t lane_max, uint32_t wave_stage) {
+                                                                           const uint32_t* __restrict__ crc_tab,
+                                                                           uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;                                           // 2048 * R dwords (slice-by-8)
-  uint16_t* ord = reinterpret_cast<uint16_t*>(lds + 2048 * R);   // [n_slots][kLaneBlock]
-  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * kLaneBlock * 2u + 15u) & ~15u);
+  uint32_t* tab = lds;                                                        // 2048 * R dwords (slice-by-8)
+  uint32_t* cnt = lds + 2048 * R;                                             // [n_slots][kLaneBlock]
+  const uint32_t S = sc.n_slots;
+  const uint32_t cnt_words = GORD ? 0u : S * kLaneBlock;
+  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneBlock]
+  const uint32_t ord_bytes = GORD ? 0u : ((S * kLaneBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage_all = reinterpret_cast<uint8_t*>(lds + 2048 * R) + ord_bytes;
+  uint8_t* stage_all = reinterpret_cast<uint8_t*>(ord) + ord_bytes;
   uint8_t* stage = stage_all + wib * kStageStride;
-  // key table for the fast path (after the 4 wave stages)
-  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
-  uint32_t* krec = kht + kLdsMaxHt;
+  uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   for (uint32_t i = threadIdx.x; i < 2048u * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
@@ -1084,11 +1119,10 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
 
   for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
        base += (uint64_t)gridDim.x * kLaneBlock) {
-    PHASE_MARK(t0);
     const uint64_t ri = base + lane;
     const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
-    RecView v;
+    RecView v{};
     bool mine = false;
     if (valid) {
       v = rec_view(B, r);
@@ -1105,36 +1139,91 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       mine = !big;
     }
     // wave-uniform staging decision over the span of this wave's records
-    const bool span_rec = mine && v.status == TFRG_OK;
-    const uint64_t lo = wave_min_u64(span_rec ? v.st : ~0ull);
-    const uint64_t hi = wave_max_u64(span_rec ? v.e : 0ull);
+    const bool span_rec = fast_ok && mine && v.status == TFRG_OK;
+    uint64_t lo, hi;
+    wave_span(span_rec, v.st, v.e, lo, hi);
     const uint64_t lo16 = lo & ~15ull;
     const bool staged = hi > lo && hi - lo16 <= kStageBytes;
     if (staged) {
       stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
-    PHASE_MARK(t1);
-    PHASE_ADD(16, t0, t1);
-    if (mine) {
-      int64_t aux = 0;
-      CountSink sink{&sc, &o, GORD ? o.order + r : ord + threadIdx.x, GORD ? B.n : (uint32_t)kLaneBlock, 0,
-                     B.n, r, v.p0, false, true};
-      int status = v.status;
-      if (status == TFRG_OK) {
-        status = staged ? count_one<R, COMPAT, true>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux)
-                        : count_one<R, COMPAT, false>(B, sc, r, v, sink, T, stage, lo16, K, fast_ok, aux);
+    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
+                           GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
+    if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
+    bool done = false;
+    if (staged && span_rec) {
+      frame_verdicts<R, true>(B, v, T, stage, lo16);
+      for (uint32_t k = 0; k < S; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+      const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+      done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+    }
+    // everything else of this wave's lane records goes to the exact walker
+    const bool slow = mine && !done;
+    const uint64_t sm = __ballot(slow);
+    if (sm) {
+      uint32_t b0 = 0;
+      if (lane == (uint32_t)__builtin_ctzll(sm)) b0 = atomicAdd(&o.info[kInfoSlow], (uint32_t)__popcll(sm));
+      b0 = __shfl(b0, __builtin_ctzll(sm), 64);
+      if (slow) o.slow_list[b0 + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = r;
+    }
+    if (done) {
+      o.status[r] = TFRG_OK;
+      o.verdict[r] = (uint8_t)v.verdict;
+    }
+    // order / count columns of the accepted records + the tile sums (one atomic per slot and wave)
+    const uint32_t tile = (uint32_t)(base >> kTileShift);
+    for (uint32_t k = 0; k < S; ++k) {
+      const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
+      const uint32_t c = ov ? sink.count_of(k) : 0u;
+      if (done) {
+        const size_t at = (size_t)k * B.n + r;
+        o.order[at] = (uint16_t)ov;
+        o.count[at] = c;
       }
-      PHASE_MARK(t3);
-      sink.finalize(status == TFRG_OK);
-      record_result(o, r, status, aux, v.verdict);
-      PHASE_MARK(t4);
-      PHASE_ADD(19, t3, t4);
+      const uint32_t x = c & ~kCountInline;
+      if (__ballot(x != 0u)) {
+        const uint32_t t = wave_sum_u32(x);
+        if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
+      }
     }
     wave_lds_sync();  // the stage is rewritten by the next iteration
-    PHASE_MARK(t2);
-    PHASE_ADD(20, t0, t2);
-    PHASE_ADD(18, t1, t2);
+  }
+}
+
+// Exact reference walk (decoder.pyx:107-300 in its own level-by-level error precedence), one lane per
+// record of the slow list, reading the record from HBM; also the framing errors and schema misses.
+template <int R, bool COMPAT, bool GORD>
+__global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema sc, DevOut o,
+                                                           const uint32_t* __restrict__ crc_tab) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t nslow = o.info[kInfoSlow];
+  if (blockIdx.x * kLaneBlock >= nslow) return;  // block-uniform
+  uint32_t* tab = lds;                            // 2048 * R dwords (slice-by-8 set; step4 uses 0..3)
+  uint32_t* cnt = lds + 2048 * R;
+  const uint32_t S = sc.n_slots;
+  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + (GORD ? 0u : S * kLaneBlock));
+  for (uint32_t i = threadIdx.x; i < 2048u * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  __syncthreads();
+  const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
+  for (uint32_t i = blockIdx.x * kLaneBlock + threadIdx.x; i < nslow; i += gridDim.x * kLaneBlock) {
+    const uint32_t r = o.slow_list[i];
+    RecView v = rec_view(B, r);
+    int64_t aux = 0;
+    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
+                           GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
+    if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
+    int status = v.status;
+    if (status == TFRG_OK) {
+      frame_verdicts<R, false>(B, v, T, nullptr, 0);
+      sink.reset();
+      Src s;
+      s.init(B.bytes, v.p0, v.L);
+      status = walk_example<COMPAT>(s, sink, aux);
+      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+    }
+    sink.finalize(status == TFRG_OK);
+    record_result(o, r, status, aux, v.verdict);
   }
 }
 
@@ -1229,15 +1318,23 @@ __device__ __forceinline__ bool entry_fast(const FastSrc& s, const LdsKeys& K, u
   return slot >= 0;
 }
 
-// Finalize of a wavefront record: order/count columns, one slot per lane.
+// Finalize of a wavefront record: order/count columns and tile sums, one slot per lane. Counts come
+// from the wave's LDS dict, or (GORD) from the count column written by other lanes of this wave.
 template <class Sink>
 __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink, uint32_t n_slots, uint32_t n,
                                               uint32_t r, bool good, uint32_t lane) {
+  if constexpr (!Sink::kLds) __threadfence();
   for (uint32_t k = lane; k < n_slots; k += 64) {
     const uint32_t vv = good ? sink.ord[(size_t)k * sink.ostride] : 0u;
     const size_t at = (size_t)k * n + r;
+    uint32_t c = 0;
+    if (vv) {
+      if constexpr (Sink::kLds) c = sink.cnt[(size_t)k * sink.ostride];
+      else c = __hip_atomic_load(&o.count[at], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     o.order[at] = (uint16_t)vv;
-    if (!vv) o.count[at] = 0;
+    o.count[at] = c;
+    if (c & ~kCountInline) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + (r >> kTileShift)], c & ~kCountInline);
   }
 }
 
@@ -1251,7 +1348,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
   uint32_t* A = lds + 1024;  // [4][256] (x) x^8192
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t ord_words = (sc.n_slots + 7u) / 8u * 4u;
-  uint16_t* word = reinterpret_cast<uint16_t*>(lds + 2048 + wib * ord_words);
+  const uint32_t wave_words = GORD ? 0u : ord_words + (sc.n_slots + 3u) / 4u * 4u;  // ord u16 + count u32
+  uint16_t* word = reinterpret_cast<uint16_t*>(lds + 2048 + wib * wave_words);
+  uint32_t* wcnt = lds + 2048 + wib * wave_words + ord_words;
   for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
@@ -1262,7 +1361,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
     const uint32_t r = o.big_list[B.n - 1u - i];
     RecView v = rec_view(B, r);
     int64_t aux = 0;
-    CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
+    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
+                           lane == 0};
+    if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
     if (framed) {
       const uint64_t D = v.e - v.st;
       if (D >= 8) {
@@ -1366,12 +1467,14 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchem
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   uint8_t* per_wave = reinterpret_cast<uint8_t*>(krec + kLdsMaxKeys * kKrWords);
   const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * 2u + 15u) & ~15u);
-  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes;
+  const uint32_t cnt_bytes = GORD ? 0u : ((sc.n_slots * 4u + 15u) & ~15u);
+  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes + cnt_bytes;
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage = per_wave + wib * wave_bytes;
   uint32_t* ent = reinterpret_cast<uint32_t*>(stage + kWStageStride);  // (len << 16) | off
   uint32_t* kmark = reinterpret_cast<uint32_t*>(ent + kMaxEnt);
   uint16_t* word = reinterpret_cast<uint16_t*>(kmark + kLdsMaxKeys);
+  uint32_t* wcnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(word) + ord_bytes);
   for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
   for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   if (fast_ok) {
@@ -1416,7 +1519,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchem
 
     PHASE_MARK(t1);
     int64_t aux = 0;
-    CountSink sink{&sc, &o, GORD ? o.order + r : word, GORD ? B.n : 1u, 0, B.n, r, v.p0, false, lane == 0};
+    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
+                           lane == 0};
+    if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
     if (framed) {
       const uint64_t D = v.e - v.st;
       const uint32_t o0 = (uint32_t)(v.st - lo16);
@@ -1473,7 +1578,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchem
           }
           sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(j + 1);  // rank = entry position
           const size_t at = (size_t)slot * B.n + r;
-          o.count[at] = cnt;
+          if constexpr (!GORD) sink.cnt[(size_t)slot * sink.ostride] = cnt;
+          else o.count[at] = cnt;
           o.loc[at] = make_uint2(lo, ll);
         }
       }
@@ -1504,127 +1610,84 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchem
 }
 
 // ------------------------------------------------------------------------------------------------
-// Per-slot exclusive scan of the counts: reduce -> spine -> downsweep. Fully parallel (no
-// inter-workgroup waiting); counts are read twice, row splits written once.
-// Tile = kScanBlock threads x kScanItems consecutive u32 per thread (16-byte loads).
+// Row-split scan, second level: per slot, exclusive scan of the 256-record tile sums in place (one
+// 1024-thread workgroup per slot, 16 tiles per thread per pass). The last workgroup to finish
+// derives the per-kind column bases from the slot totals.
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* s_w, uint32_t& total) {
-  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  uint32_t incl = v;
+constexpr int kSpineBlock = 1024;
+constexpr int kSpineItems = 16;
+
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= (uint32_t)d) incl += y;
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += y;
   }
-  if (lane == 63) s_w[wid] = incl;
-  __syncthreads();
-  uint32_t pre = 0, tot = 0;
-#pragma unroll
-  for (int w = 0; w < kScanBlock / 64; ++w) {
-    const uint32_t x = s_w[w];
-    pre += (uint32_t)w < wid ? x : 0u;
-    tot += x;
-  }
-  __syncthreads();
-  total = tot;
-  return pre + incl - v;
+  return v;
 }
 
-__device__ __forceinline__ void load_items(const uint32_t* c, uint64_t base, uint32_t n, uint32_t (&v)[kScanItems]) {
-  if (base + kScanItems <= n && ((base & 3u) == 0)) {
-#pragma unroll
-    for (int i = 0; i < kScanItems; i += 4) {
-      const uint4 q = *reinterpret_cast<const uint4*>(c + base + i);
-      v[i] = q.x;
-      v[i + 1] = q.y;
-      v[i + 2] = q.z;
-      v[i + 3] = q.w;
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kScanItems; ++i) v[i] = base + i < n ? c[base + i] : 0u;
-  }
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) v[i] &= ~kCountInline;
-}
-
-// phase 1: per-tile sums -> tsum[slot][tile]
-__global__ __launch_bounds__(kScanBlock) void k_scan_reduce(const uint32_t* __restrict__ count, uint32_t* tsum,
-                                                            uint32_t n, uint32_t n_tiles) {
-  __shared__ uint32_t s_w[kScanBlock / 64];
-  const uint32_t slot = blockIdx.y, tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
-  load_items(count + (size_t)slot * n, base, n, v);
-  uint32_t sum = 0;
-#pragma unroll
-  for (int i = 0; i < kScanItems; ++i) sum += v[i];
-  uint32_t total;
-  block_excl_scan(sum, s_w, total);
-  if (threadIdx.x == 0) tsum[(size_t)slot * n_tiles + tile] = total;
-}
-
-// phase 2: exclusive scan of the tile sums of one slot (one workgroup per slot)
-__global__ __launch_bounds__(kScanBlock) void k_scan_spine(uint32_t* tsum, uint32_t* totals, uint32_t n_tiles) {
-  __shared__ uint32_t s_w[kScanBlock / 64];
-  uint32_t* t = tsum + (size_t)blockIdx.x * n_tiles;
+__global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* __restrict__ slot_kind, uint32_t n_slots,
+                                                       uint32_t n_tiles) {
+  __shared__ uint32_t s_w[kSpineBlock / 64];
+  __shared__ uint32_t s_last;
+  const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
+  uint32_t* t = o.tsum + (size_t)blockIdx.x * o.tile_stride;
   uint32_t carry = 0;
-  for (uint32_t b = 0; b < n_tiles; b += kScanBlock) {
-    const uint32_t i = b + threadIdx.x;
-    const uint32_t v = i < n_tiles ? t[i] : 0u;
-    uint32_t total;
-    const uint32_t ex = block_excl_scan(v, s_w, total);
-    if (i < n_tiles) t[i] = carry + ex;
-    carry += total;
-  }
-  if (threadIdx.x == 0) totals[blockIdx.x] = carry;
-}
-
-// phase 3: row splits = tile prefix + in-tile exclusive scan
-__global__ __launch_bounds__(kScanBlock) void k_scan_down(const uint32_t* __restrict__ count, uint32_t* rs,
-                                                          const uint32_t* __restrict__ tsum,
-                                                          const uint32_t* __restrict__ totals, uint32_t n,
-                                                          uint32_t n_tiles) {
-  __shared__ uint32_t s_w[kScanBlock / 64];
-  const uint32_t slot = blockIdx.y, tile = blockIdx.x;
-  const uint64_t base = (uint64_t)tile * kScanTile + (uint64_t)threadIdx.x * kScanItems;
-  uint32_t v[kScanItems];
-  load_items(count + (size_t)slot * n, base, n, v);
-  uint32_t sum = 0;
+  for (uint32_t b = 0; b < n_tiles; b += kSpineBlock * kSpineItems) {
+    const uint32_t i0 = b + threadIdx.x * kSpineItems;
+    uint32_t v[kSpineItems];
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) sum += v[i];
-  uint32_t total;
-  uint32_t run = tsum[(size_t)slot * n_tiles + tile] + block_excl_scan(sum, s_w, total);
-  uint32_t* out = rs + (size_t)slot * (n + 1);
-  uint32_t w[kScanItems];
+    for (int j = 0; j < kSpineItems; j += 4) {  // tile_stride is a multiple of 4: whole uint4s are in bounds
+      uint4 q = make_uint4(0, 0, 0, 0);
+      if (i0 + j < n_tiles) q = *reinterpret_cast<const uint4*>(t + i0 + j);
+      v[j] = q.x;
+      v[j + 1] = i0 + j + 1 < n_tiles ? q.y : 0u;
+      v[j + 2] = i0 + j + 2 < n_tiles ? q.z : 0u;
+      v[j + 3] = i0 + j + 3 < n_tiles ? q.w : 0u;
+    }
+    uint32_t sum = 0;
 #pragma unroll
-  for (int i = 0; i < kScanItems; ++i) {
-    w[i] = run;
-    run += v[i];
-  }
-  const uint64_t gaddr = (size_t)slot * (n + 1) + base;  // element index of out[base] in rs
-  if (base + kScanItems <= n && (gaddr & 3u) == 0) {
+    for (int j = 0; j < kSpineItems; ++j) sum += v[j];
+    const uint32_t incl = wave_incl_scan_u32(sum, lane);
+    if (lane == 63) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t pre = carry, tot = 0;
 #pragma unroll
-    for (int i = 0; i < kScanItems; i += 4)
-      *reinterpret_cast<uint4*>(out + base + i) = make_uint4(w[i], w[i + 1], w[i + 2], w[i + 3]);
-  } else {
+    for (int w = 0; w < kSpineBlock / 64; ++w) {
+      const uint32_t x = s_w[w];
+      pre += (uint32_t)w < wid ? x : 0u;
+      tot += x;
+    }
+    __syncthreads();
+    uint32_t run = pre + incl - sum;
 #pragma unroll
-    for (int i = 0; i < kScanItems; ++i)
-      if (base + i < n) out[base + i] = w[i];
+    for (int j = 0; j < kSpineItems; j += 4) {
+      uint32_t w[4];
+#pragma unroll
+      for (int m = 0; m < 4; ++m) {
+        w[m] = run;
+        run += v[j + m];
+      }
+      if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    carry += tot;
   }
-  if (tile == 0 && threadIdx.x == 0) out[n] = totals[slot];
-}
-
-__global__ void k_base(const uint32_t* totals, const uint8_t* slot_kind, uint64_t* slot_base,
-                       uint64_t* kind_totals, uint32_t n_slots) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  uint64_t acc[4] = {0, 0, 0, 0};
-  for (uint32_t s = 0; s < n_slots; ++s) {
-    const uint32_t k = slot_kind[s] & 3u;
-    slot_base[s] = acc[k];
-    acc[k] += totals[s];
+  if (threadIdx.x == 0) {
+    o.totals[blockIdx.x] = carry;
+    __threadfence();
+    s_last = atomicAdd(&o.info[kInfoSpineDone], 1u) == n_slots - 1u;
   }
-  for (int k = 0; k < 4; ++k) kind_totals[k] = acc[k];
+  __syncthreads();
+  if (s_last && threadIdx.x == 0) {  // every slot total is visible: column bases per kind
+    __threadfence();
+    uint64_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t s = 0; s < n_slots; ++s) {
+      const uint32_t k = slot_kind[s] & 3u;
+      o.slot_base[s] = acc[k];
+      acc[k] += __hip_atomic_load(&o.totals[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1726,82 +1789,141 @@ __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2
   }
 }
 
+// Row-split scan, last level, fused with the lane-record gather. One workgroup per 256-record tile:
+// per slot, the tile prefix (k_spine) + the in-tile exclusive scan of the counts give the row splits;
+// single values kept inline by the count pass are written straight from the loc word, other lists of
+// records <= lane_max are decoded from the wave's LDS stage. Records above lane_max belong to the
+// wavefront gather kernels, which run next and read these row splits.
+constexpr uint32_t kDG = 2;   // slots per scan group
+// kDT tiles per workgroup: kDT x kDG (count, loc) loads in flight per thread (4 for large batches,
+// 1 when that would leave CUs idle)
+
+template <bool COMPAT, uint32_t kDT>
+__global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max,
+                                                            uint32_t n_tiles) {
+  __shared__ uint32_t s_w[2][kDT * kDG][4];  // wave totals, double-buffered across slot groups
+  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t S = sc.n_slots;
+  if (blockIdx.x == 0)
+    for (uint32_t k = threadIdx.x; k < S; k += kLaneBlock) o.rs[(size_t)k * (B.n + 1) + B.n] = o.totals[k];
+  const uint32_t tile0 = blockIdx.x * kDT;
+  uint32_t r[kDT];
+  bool valid[kDT];
+#pragma unroll
+  for (uint32_t t = 0; t < kDT; ++t) {
+    r[t] = ((tile0 + t) << kTileShift) + threadIdx.x;
+    valid[t] = r[t] < B.n;
+  }
+  // row splits of every slot + inline single values. A non-zero count implies a decoded record
+  // with the slot present (failed records and absent slots have count 0).
+  uint32_t need = 0;  // bit t: record r[t] has an out-of-line list
+  uint32_t buf = 0;
+  for (uint32_t k0 = 0; k0 < S; k0 += kDG, buf ^= 1u) {
+    uint32_t c[kDT][kDG], ex[kDT][kDG];
+    uint2 lc[kDT][kDG];
+#pragma unroll
+    for (uint32_t t = 0; t < kDT; ++t) {  // every load of the group issued before the barrier
+#pragma unroll
+      for (uint32_t g = 0; g < kDG; ++g) {
+        const uint32_t k = k0 + g < S ? k0 + g : k0;
+        const bool in = valid[t] && k0 + g < S;
+        c[t][g] = in ? o.count[(size_t)k * B.n + r[t]] : 0u;
+        lc[t][g] = in ? o.loc[(size_t)k * B.n + r[t]] : make_uint2(0, 0);
+      }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < kDT; ++t) {
+#pragma unroll
+      for (uint32_t g = 0; g < kDG; ++g) {
+        const uint32_t x = c[t][g] & ~kCountInline;
+        const uint32_t incl = wave_incl_scan_u32(x, lane);
+        ex[t][g] = incl - x;
+        if (lane == 63) s_w[buf][t * kDG + g][wib] = incl;
+      }
+    }
+    __syncthreads();  // (the other buffer is rewritten only after the next group's barrier)
+#pragma unroll
+    for (uint32_t g = 0; g < kDG; ++g) {
+      const uint32_t k = k0 + g;
+      if (k >= S) break;
+      const uint32_t kind = sc.slot_kind[k];
+      const uint64_t sbase = o.slot_base[k];
+#pragma unroll
+      for (uint32_t t = 0; t < kDT; ++t) {
+        if (tile0 + t >= n_tiles) break;
+        uint32_t pre = o.tsum[(size_t)k * o.tile_stride + tile0 + t];
+        for (uint32_t w = 0; w < wib; ++w) pre += s_w[buf][t * kDG + g][w];
+        const uint32_t rsv = pre + ex[t][g];
+        if (valid[t]) o.rs[(size_t)k * (B.n + 1) + r[t]] = rsv;
+        if (c[t][g] & kCountInline) put_inline(o, kind, lc[t][g], sbase + rsv);
+        else if (c[t][g]) need |= 1u << t;
+      }
+    }
+  }
+  // records with an out-of-line list: k_list_gather (kept out of this kernel so its register
+  // budget stays that of the scan); larger records are skipped there (wavefront gathers)
+#pragma unroll
+  for (uint32_t t = 0; t < kDT; ++t) {
+    const bool nd = (need >> t) & 1u;
+    const uint64_t nm = __ballot(nd);
+    if (nm) {
+      const int f = __builtin_ctzll(nm);
+      uint32_t b0 = 0;
+      if (lane == (uint32_t)f) b0 = atomicAdd(&o.info[kInfoNeed], (uint32_t)__popcll(nm));
+      b0 = __shfl(b0, f, 64);
+      if (nd) o.slow_list[b0 + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull))] = r[t];
+    }
+  }
+}
+
+// Out-of-line lists of lane records (k_down_gather's list; lane order within a wave, so the records
+// of a wave are usually one contiguous span): staged in LDS and decoded by their own lane.
 template <bool COMPAT>
-__global__ __launch_bounds__(kLaneBlock) void k_lane_gather(DevBatch B, DevSchema sc, DevOut o,
-                                                            uint32_t lane_max) {
+__global__ __launch_bounds__(kLaneBlock) void k_list_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kStageStride;
-  for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
-       base += (uint64_t)gridDim.x * kLaneBlock) {
-    const uint64_t ri = base + lane;
-    const uint32_t r = (uint32_t)ri;
-    // pass 1: slot metadata (every load issued up front); inline single values written now. A
-    // non-zero count implies a decoded record with the slot present (failed records and absent
-    // slots have count 0), so neither status nor order is read.
-    bool need = false;
-    if (ri < B.n) {
-      for (uint32_t k0 = 0; k0 < sc.n_slots; k0 += 4) {
-        uint32_t cntv[4], rsv[4];
-        uint2 lcv[4];
-        uint64_t basev[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t k = k0 + j < sc.n_slots ? k0 + j : k0;
-          const size_t at = (size_t)k * B.n + r;
-          cntv[j] = o.count[at];
-          lcv[j] = o.loc[at];
-          rsv[j] = o.rs[(size_t)k * (B.n + 1) + r];
-          basev[j] = o.slot_base[k];
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const uint32_t k = k0 + j;
-          if (k >= sc.n_slots || !cntv[j]) continue;
-          if (cntv[j] & kCountInline) put_inline(o, sc.slot_kind[k], lcv[j], basev[j] + rsv[j]);
-          else need = true;
-        }
-      }
+  const uint32_t nneed = o.info[kInfoNeed];
+  const uint32_t S = sc.n_slots;
+  for (uint32_t base = blockIdx.x * kLaneBlock + wib * 64u; base < nneed; base += gridDim.x * kLaneBlock) {
+    const uint32_t i = base + lane;
+    bool need = i < nneed;
+    const uint32_t r = need ? o.slow_list[i] : 0u;
+    RecView v{};
+    if (need) {
+      v = rec_view(B, r);
+      need = v.e - v.st <= lane_max;  // larger records belong to the wavefront gather kernels
     }
-    // pass 2 (only when some record of the wave has an out-of-line list): stage and decode;
-    // records above lane_max belong to the wavefront gather kernels
-    if (__ballot(need)) {
-      RecView v;
-      if (need) {
-        v = rec_view(B, r);
-        need = v.e - v.st <= lane_max;
-      }
-      uint64_t lo, hi;
-      wave_span(need, v.st, v.e, lo, hi);
-      const uint64_t lo16 = lo & ~15ull;
-      const bool staged = hi > lo && hi - lo16 <= kStageBytes;
-      if (staged) {
-        stage_span(stage, B.bytes, lo16, hi, lane);
-        wave_lds_sync();
-      }
-      if (need) {
-        if (staged) {
-          const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-          LdsSrc s;
-          s.init(stage, lo16, v.p0, v.L);
-          for (uint32_t k = 0; k < sc.n_slots; ++k) {
-            const size_t at = (size_t)k * B.n + r;
-            const uint32_t c = o.count[at];
-            if (!c || (c & kCountInline)) continue;
-            const uint2 lc = o.loc[at];
-            const uint32_t kind = sc.slot_kind[k];
-            const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
-            if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
-              list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
-          }
-        } else {
-          Src s;
-          s.init(B.bytes, v.p0, v.L);
-          gather_record<COMPAT>(B, sc, o, r, s);
-        }
-      }
+    uint64_t lo, hi;
+    wave_span(need, v.st, v.e, lo, hi);
+    const uint64_t lo16 = lo & ~15ull;
+    const bool staged = hi > lo && hi - lo16 <= kStageBytes;
+    if (staged) {
+      stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
+    if (need) {
+      if (staged) {
+        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+        LdsSrc s;
+        s.init(stage, lo16, v.p0, v.L);
+        for (uint32_t k = 0; k < S; ++k) {
+          const size_t at = (size_t)k * B.n + r;
+          const uint32_t c = o.count[at];
+          if (!c || (c & kCountInline)) continue;
+          const uint2 lc = o.loc[at];
+          const uint32_t kind = sc.slot_kind[k];
+          const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
+          if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
+            list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
+        }
+      } else {
+        Src s;
+        s.init(B.bytes, v.p0, v.L);
+        gather_record<COMPAT>(B, sc, o, r, s);
+      }
+    }
+    wave_lds_sync();
   }
 }
 
@@ -1948,12 +2070,15 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
 // ------------------------------------------------------------------------------------------------
 // launcher
 // ------------------------------------------------------------------------------------------------
-constexpr int kLaneRep = 2;  // CRC table bank replication in the lane kernel (slice-by-8: 16 KiB)
+constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (slice-by-8: 8 KiB per copy)
 
-constexpr size_t kLdsBudget = 128 * 1024;  // above this the dict state goes to the global column
+constexpr size_t kLdsBudget = 128 * 1024;     // wavefront kernels: above this the dict goes to the columns
+constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count", "k_wave_count", "k_scan",
-                                             "k_base",       "k_lane_gather", "k_wave_gather"};
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_slow_count",  "k_wave_count", "k_spine",
+                                             "k_down_gather", "k_list_gather", "k_wave_gather"};
+
+static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 template <bool COMPAT>
 static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
@@ -1961,30 +2086,53 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   auto mark = [&](int i) {
     if (ev) (void)hipEventRecord(ev[i], st);
   };
+  const size_t S = sc.n_slots;
+  const uint32_t n_tiles = (b.n + kTileRecs - 1) / kTileRecs;
+  const size_t dict_lane = S * kLaneBlock * 4 + r16(S * kLaneBlock * 2);  // cnt u32 + ord u16 per lane
   const size_t tab_lds = 2048ull * kLaneRep * 4;
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
   const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
-                              ? (kLdsMaxHt + (size_t)sc.n_keys * kKrWords) * 4 : 0;
-  const size_t lane_lds = tab_lds + (((size_t)sc.n_slots * kLaneBlock * 2 + 15) & ~(size_t)15) + stage_lds + keys_lds;
+                              ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
+  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds;
+  const size_t slow_lds = 2048ull * 4 + dict_lane;
   const size_t wave_shared = (2048ull + 128 + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
   const size_t wave_per = (size_t)kWStageStride + kMaxEnt * 4 + kLdsMaxKeys * 4;
-  const size_t stage_lds_w =
-      wave_shared + kWavesPerBlock * (wave_per + (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15));
+  const size_t dict_wave = r16(S * 2) + r16(S * 4);
+  const size_t stage_lds_w = wave_shared + kWavesPerBlock * (wave_per + dict_wave);
   const size_t stage_lds_wg = wave_shared + kWavesPerBlock * wave_per;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
+
   mark(kStageLaneCount);
-  if (lane_lds <= kLdsBudget) {
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), lane_lds, st,
-                       b, sc, o, d_tab, cfg.lane_max, wave_stage);
+  // one round of resident workgroups (a second, partial round would idle most CUs at the tail)
+  auto resident_grid = [&](const void* fn, size_t lds) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLaneBlock, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int g = per_cu * cfg.num_cus;
+    return g < cfg.lane_grid ? g : cfg.lane_grid;
+  };
+  if (lane_lds <= kLaneLdsBudget) {
+    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, false>);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(resident_grid(fn, lane_lds)), dim3(kLaneBlock),
+                       lane_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else {
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock),
-                       tab_lds + stage_lds + keys_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+    const size_t lds = tab_lds + stage_lds + keys_lds;
+    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, true>);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
+                       st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+  }
+  mark(kStageSlowCount);
+  if (slow_lds <= kLaneLdsBudget) {
+    hipLaunchKernelGGL((k_slow_count<1, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), slow_lds, st, b, sc,
+                       o, d_tab);
+  } else {
+    hipLaunchKernelGGL((k_slow_count<1, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), 2048ull * 4, st, b,
+                       sc, o, d_tab);
   }
   mark(kStageWaveCount);
   // staged (record span <= kWStage) and huge records: two launches, the second with a small LDS
   // footprint so the streaming CRC of huge records runs at full occupancy
-  const size_t ord_lds = kWavesPerBlock * (((size_t)sc.n_slots * 2 + 15) & ~(size_t)15);
-  const size_t huge_lds = 2048ull * 4 + ord_lds;
+  const size_t huge_lds = 2048ull * 4 + kWavesPerBlock * ((S + 7) / 8 * 16 + (S + 3) / 4 * 16);
   if (stage_lds_w <= kLdsBudget) {
     hipLaunchKernelGGL((k_stage_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_w, st, b,
                        sc, o, d_tab, d_consts);
@@ -1999,24 +2147,23 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b,
                        sc, o, d_tab, d_consts);
   }
-  mark(kStageScan);
-  if (sc.n_slots > 0) {
-    const uint32_t n_tiles = (b.n + kScanTile - 1) / kScanTile;
-    const dim3 grid(n_tiles, sc.n_slots);
-    hipLaunchKernelGGL(k_scan_reduce, grid, dim3(kScanBlock), 0, st, o.count, o.tsum, b.n, n_tiles);
-    hipLaunchKernelGGL(k_scan_spine, dim3(sc.n_slots), dim3(kScanBlock), 0, st, o.tsum, o.totals, n_tiles);
-    hipLaunchKernelGGL(k_scan_down, grid, dim3(kScanBlock), 0, st, o.count, o.rs, o.tsum, o.totals, b.n, n_tiles);
+  mark(kStageSpine);
+  if (S > 0) hipLaunchKernelGGL(k_spine, dim3(S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
+  mark(kStageDownGather);
+  if (S > 0) {
+    if (n_tiles >= 16u * (uint32_t)cfg.num_cus)
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3((n_tiles + 3) / 4), dim3(kLaneBlock), 0, st, b, sc, o,
+                         cfg.lane_max, n_tiles);
+    else
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles), dim3(kLaneBlock), 0, st, b, sc, o, cfg.lane_max,
+                         n_tiles);
   }
-  mark(kStageBase);
-  hipLaunchKernelGGL(k_base, dim3(1), dim3(64), 0, st, o.totals, sc.slot_kind, o.slot_base, o.kind_totals,
-                     sc.n_slots);
-  mark(kStageLaneGather);
-  if (sc.n_slots > 0) {
-    hipLaunchKernelGGL((k_lane_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
+  mark(kStageListGather);
+  if (S > 0)
+    hipLaunchKernelGGL((k_list_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
                        cfg.lane_max);
-  }
   mark(kStageWaveGather);
-  if (sc.n_slots > 0) {
+  if (S > 0) {
     hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock),
                        (size_t)kWStageStride * kWavesPerBlock, st, b, sc, o);
     hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
