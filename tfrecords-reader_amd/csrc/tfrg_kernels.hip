@@ -917,7 +917,7 @@ __device__ __forceinline__ int fast_lookup(const FastSrc& s, const LdsKeys& K, u
   return -1;
 }
 
-// Returns TFRG_OK with the dict in sink.ord / count / loc, or kBail.
+// One packed int64 varint at `pos` of a validated chunk ending at `e` (fast gather path); false = bail.
 template <bool COMPAT>
 __device__ __forceinline__ bool fast_value(const FastSrc& s, uint32_t& pos, uint32_t e, int64_t& val) {
   const uint32_t w = s.w4(pos);
@@ -984,56 +984,111 @@ __device__ __forceinline__ bool fast_single(const FastSrc& s, uint32_t kind, uin
   return true;
 }
 
+
+// Branch-free header of a length-delimited field at `pos` inside [pos, end): 1-byte tag with wire
+// type 2, 1..3-byte length, body inside `end`. Anything else is not canonical (ok = false); the
+// outputs are then garbage but positions stay inside the record, so the caller may keep computing
+// and decide once.
+__device__ __forceinline__ bool hdr2(const FastSrc& s, uint32_t pos, uint32_t end, uint32_t& fn, uint32_t& off,
+                                     uint32_t& len) {
+  pos = pos < s.L ? pos : s.L;
+  const uint32_t w = lds_u32u(s.l, s.p + pos);
+  const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
+  const uint32_t c1 = b1 >> 7, c12 = c1 & (b2 >> 7);
+  uint32_t l = b1 & 0x7fu;
+  l |= c1 ? (b2 & 0x7fu) << 7 : 0u;
+  l |= c12 ? b3 << 14 : 0u;
+  fn = (w >> 3) & 0xfu;
+  off = pos + 2u + c1 + c12;
+  len = l;
+  return ((w & 0x87u) == 0x02u) & !(c12 & (b3 >> 7)) & (off <= end) & (l <= end - off);
+}
+
+// Returns TFRG_OK with the dict in sink.ord / cnt (or count) / loc, or kBail (exact walker).
+// Every level is a single canonical pass: one Features field spanning the Example, map entries of
+// exactly (key #1, value #2), one kind field spanning the Feature, list chunks of field #1.
 template <bool COMPAT, class Sink>
 __device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Sink& sink) {
-  uint32_t pos = 0;
   const uint32_t L = s.L;
-  bool have = false;
+  uint32_t fn, fo, fl;
+  bool ok = hdr2(s, 0, L, fn, fo, fl) & (fn == 1u) & (fo + fl == L);
   uint64_t seen = 0;  // key ids < 64 already in the dict (a duplicate key bails)
-  while (pos < L) {
-    uint32_t fn, fo, fl;
-    if (have || !ffield(s, pos, L, fn, fo, fl) || fn != 1u) return kBail;
-    have = true;
-    uint32_t q = fo;
-    const uint32_t fe = fo + fl;
-    while (q < fe) {
-      uint32_t en, eo, el;
-      if (!ffield(s, q, fe, en, eo, el) || en != 1u) return kBail;
-      uint32_t e = eo;
-      const uint32_t ee = eo + el;
-      uint32_t kn, ko, kl, vn, vo, vl;
-      if (!ffield(s, e, ee, kn, ko, kl) || kn != 1u) return kBail;
-      if (!ffield(s, e, ee, vn, vo, vl) || vn != 2u || e != ee) return kBail;
-      const int kid = fast_lookup(s, K, ko, kl);
-      if (kid < 0) return kBail;
-      const uint32_t* kr = K.rec + (uint32_t)kid * kKrWords;
-      uint32_t g = vo, kind, lo, ll, cnt;
-      if (!ffield(s, g, vo + vl, kind, lo, ll) || g != vo + vl || kind < 1u || kind > 3u) return kBail;
-      if (!fast_list_count(s, kind, lo, ll, cnt)) return kBail;
-      const int slot = (int)kr[kKrSlot1 + kind - 1];
-      if (slot < 0) return kBail;
-      if (kid < 64) {
-        const uint64_t bit = 1ull << kid;
-        if (seen & bit) return kBail;
-        seen |= bit;
-      } else {
-        for (int k = 0; k < 3; ++k) {
-          const int s2 = (int)kr[kKrSlot1 + k];
-          if (s2 >= 0 && sink.ord[(size_t)s2 * sink.ostride]) return kBail;
-        }
+  uint32_t rank = 0;
+  const uint32_t fe = fo + fl;
+  for (uint32_t q = fo; ok && q < fe;) {
+    uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
+    ok = hdr2(s, q, fe, en, eo, el) & (en == 1u);
+    const uint32_t ee = eo + el;
+    q = ee;
+    ok &= hdr2(s, eo, ee, kn, ko, kl) & (kn == 1u);
+    ok &= hdr2(s, ko + kl, ee, vn, vo, vl) & (vn == 2u) & (vo + vl == ee);
+    ok &= hdr2(s, vo, ee, kind, lo, ll) & (lo + ll == ee) & (kind - 1u < 3u);
+    if (!ok) break;
+    const int kid = fast_lookup(s, K, ko, kl);
+    // list chunks (field #1, packed); the first chunk's single value is kept for the inline path
+    uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0;
+    const uint32_t le = lo + ll;
+    for (uint32_t g = lo; ok && g < le;) {
+      uint32_t cf, co, cl;
+      ok = hdr2(s, g, le, cf, co, cl) & (cf == 1u);
+      g = co + cl;
+      if (nch == 0) {
+        c0o = co;
+        c0l = cl;
       }
-      if (sink.rank >= 65534u) return kBail;
-      sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(++sink.rank);
-      const size_t at = (size_t)slot * sink.n + sink.r;
-      uint2 lv = make_uint2(lo, ll);
-      uint32_t cw = cnt;
-      if (cnt == 1u && fast_single<COMPAT>(s, kind, lo, ll, lv)) cw = 1u | kCountInline;
-      if constexpr (Sink::kLds) sink.cnt[(size_t)slot * sink.ostride] = cw;
-      else sink.o->count[at] = cw;
-      sink.o->loc[at] = lv;
+      ++nch;
+      if (kind == TFRG_KIND_BYTES) {
+        ++cnt;
+      } else if (kind == TFRG_KIND_FLOAT) {
+        ok &= (cl & 3u) == 0u;
+        cnt += cl >> 2;
+      } else {
+        uint32_t k = 0;
+        ok &= count_packed(s, co, co + cl, k);
+        cnt += k;
+      }
     }
+    ok &= kid >= 0;
+    if (!ok) break;
+    const uint32_t* kr = K.rec + (uint32_t)kid * kKrWords;
+    const int slot = (int)kr[kKrSlot1 + kind - 1];
+    if (kid < 64) {
+      const uint64_t bit = 1ull << kid;
+      ok &= !(seen & bit);
+      seen |= bit;
+    } else {
+      for (int k = 0; k < 3; ++k) {
+        const int s2 = (int)kr[kKrSlot1 + k];
+        ok &= !(s2 >= 0 && sink.ord[(size_t)s2 * sink.ostride]);
+      }
+    }
+    ok &= (slot >= 0) & (rank < 65534u);
+    if (!ok) break;
+    sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(++rank);
+    // a single value goes inline into the loc word (int64 bits, float bits, bytes view)
+    uint2 lv = make_uint2(lo, ll);
+    uint32_t cw = cnt;
+    if (cnt == 1u && nch == 1u) {
+      if (kind == TFRG_KIND_BYTES) {
+        lv = make_uint2((uint32_t)(s.base + c0o), c0l);
+        cw = 1u | kCountInline;
+      } else if (kind == TFRG_KIND_FLOAT) {
+        lv = make_uint2(lds_u32u(s.l, s.p + c0o), 0u);
+        cw = 1u | kCountInline;
+      } else if (c0l <= 4u) {  // one varint of <= 4 bytes: value < 2^28, same in both varint modes
+        const uint32_t w = lds_u32u(s.l, s.p + c0o);
+        const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+        lv = make_uint2(x & ((1u << (7u * c0l)) - 1u), 0u);
+        cw = 1u | kCountInline;
+      }
+    }
+    const size_t at = (size_t)slot * sink.n + sink.r;
+    if constexpr (Sink::kLds) sink.cnt[(size_t)slot * sink.ostride] = cw;
+    else sink.o->count[at] = cw;
+    sink.o->loc[at] = lv;
   }
-  return have ? TFRG_OK : kBail;
+  sink.rank = rank;
+  return ok ? TFRG_OK : kBail;
 }
 
 // Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
