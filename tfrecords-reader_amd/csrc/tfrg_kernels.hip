@@ -741,6 +741,11 @@ __device__ __forceinline__ uint32_t crc_head_state(uint32_t k) {
   // ~0 (x) x^(-8k) for k = 0..3 (checked against crc32c("123456789") with k zero bytes prepended)
   return k == 0 ? 0xffffffffu : (k == 1 ? 0xa942e6bcu : (k == 2 ? 0x2804363bu : 0x96db52a8u));
 }
+#ifndef TFRG_LANE_SLICE
+#define TFRG_LANE_SLICE 4  // slicing width of the lane kernel's CRC (4: 4 KiB of tables, 8: 8 KiB)
+#endif
+constexpr int kLaneSlice = TFRG_LANE_SLICE;
+
 template <int R>
 __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<R>& T) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(l);
@@ -748,9 +753,16 @@ __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint3
   uint32_t p = a & ~3u;
   uint32_t c = crc_head_state(k);
   uint32_t hm = 0xffffffffu << (8u * k);  // masks the bytes before a in the first dword
-  for (; p + 8 <= bw; p += 8) {
-    c = T.step8(c ^ (w[p >> 2] & hm), w[(p >> 2) + 1]);
-    hm = 0xffffffffu;
+  if constexpr (kLaneSlice == 8) {
+    for (; p + 8 <= bw; p += 8) {
+      c = T.step8(c ^ (w[p >> 2] & hm), w[(p >> 2) + 1]);
+      hm = 0xffffffffu;
+    }
+  } else {  // slice-by-4: the smaller table leaves LDS for more resident waves
+    for (; p + 8 <= bw; p += 4) {
+      c = T.step4(c ^ (w[p >> 2] & hm));
+      hm = 0xffffffffu;
+    }
   }
   if (p + 4 <= bw) {
     c = T.step4(c ^ (w[p >> 2] & hm));
@@ -1151,8 +1163,8 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;                                                        // 2048 * R dwords (slice-by-8)
-  uint32_t* cnt = lds + 2048 * R;                                             // [n_slots][kLaneBlock]
+  uint32_t* tab = lds;                                       // 256 * kLaneSlice * R dwords (slicing tables)
+  uint32_t* cnt = lds + 256 * kLaneSlice * R;                // [n_slots][kLaneBlock]
   const uint32_t S = sc.n_slots;
   const uint32_t cnt_words = GORD ? 0u : S * kLaneBlock;
   uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneBlock]
@@ -1162,7 +1174,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
   uint8_t* stage = stage_all + wib * kStageStride;
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
-  for (uint32_t i = threadIdx.x; i < 2048u * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
@@ -2144,7 +2156,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t S = sc.n_slots;
   const uint32_t n_tiles = (b.n + kTileRecs - 1) / kTileRecs;
   const size_t dict_lane = S * kLaneBlock * 4 + r16(S * kLaneBlock * 2);  // cnt u32 + ord u16 per lane
-  const size_t tab_lds = 2048ull * kLaneRep * 4;
+  const size_t tab_lds = 256ull * kLaneSlice * kLaneRep * 4;
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
   const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
                               ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
