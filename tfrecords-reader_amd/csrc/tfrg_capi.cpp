@@ -107,7 +107,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   }
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (wavefront kernels), then
   // [8][256] slice-by-8 (lane kernel); consts: 64 lane shifts x^(128 l) and 16 un-shifts x^(-8z)
-  std::vector<uint32_t> tab(4096), cst(80);
+  std::vector<uint32_t> tab(5120), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -115,8 +115,11 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   crc_make_mul_tables(gf_xpow8(1024), M);
   memcpy(tab.data() + 1024, M, 4096);
   memcpy(tab.data() + 2048, T.t, 8192);
+  crc_make_mul_tables(gf_xpow8(4096), M);  // (x) x^32768: four interleaved waves of 1 KiB rounds
+  memcpy(tab.data() + 4096, M, 4096);
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
+  for (int w = 0; w < 4; ++w) cst[80 + w] = gf_xpow8(1024ull * w);  // wave w's rounds: x^(8192 w)
   if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||
       hipMemcpy(c->crc_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->consts.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {

@@ -1405,58 +1405,146 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
   }
 }
 
-// Huge records (beyond the LDS stage): streaming CRC from HBM and the wave-uniform exact walk.
+// Huge records (span beyond the LDS stage): one WORKGROUP per record. The payload CRC is split over
+// the 4 waves by interleaved 1 KiB rounds (64 lanes x 16-byte chunks, rounds counted from the end;
+// wave w takes rounds w, w+4, w+8, ...) with kHugeDepth rounds of loads in flight per lane. A lane's
+// state advances by x^32768 per step of its wave (A4 tables), wave w's lane-combined sum is shifted
+// by x^(8192 w), and the four sums XOR together (crc32c.h algebra). Wave 0 then runs the exact,
+// wave-uniform walk over the (now L2-warm) record.
+constexpr int kHugeDepth = 4;
+
+// U(0, 16-byte chunk at q) of the payload [a, b): bytes outside zeroed, the first 4 payload bytes
+// inverted (the ~0 initial state)
+__device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uint64_t b, const LdsTab<1>& T) {
+  uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  if (q < a + 4 || q + 16 > b) {
+#pragma unroll
+    for (int k2 = 0; k2 < 4; ++k2) {
+      uint32_t keep = 0, inv = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t ba = q + 4ull * k2 + j;
+        if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
+        if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
+      }
+      ws[k2] = (ws[k2] & keep) ^ inv;
+    }
+  }
+  uint32_t Rc = 0;
+#pragma unroll
+  for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
+  return Rc;
+}
+
+__device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
+  return M[S & 0xffu] ^ M[256 + ((S >> 8) & 0xffu)] ^ M[512 + ((S >> 16) & 0xffu)] ^ M[768 + (S >> 24)];
+}
+
+// this wave's share of U(0, payload') over [a, b) (b - a >= 64), lane-combined, not yet shifted
+__device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
+                                                  const uint32_t* A4, const uint32_t* cst, uint32_t w, uint32_t lane) {
+  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
+  const int64_t rounds = (c1 - c0 + 64) >> 6;
+  const int64_t J = rounds > (int64_t)w ? (rounds - (int64_t)w + 3) / 4 : 0;  // rounds w + 4j, j < J
+  uint32_t S = 0;
+  for (int64_t j = J - 1; j >= 0; j -= kHugeDepth) {  // Horner from the payload start (largest round)
+    uint4 wv[kHugeDepth];
+    int64_t chv[kHugeDepth];
+#pragma unroll
+    for (int d = 0; d < kHugeDepth; ++d) {  // every load of the group in flight before any use
+      const int64_t k = (int64_t)w + 4 * (j - d);
+      const int64_t ch = c1 - 64 * k - (int64_t)lane;
+      chv[d] = ch;
+      const bool in = j - d >= 0 && ch >= c0;
+      wv[d] = *reinterpret_cast<const uint4*>(buf + (in ? (uint64_t)ch << 4 : (a & ~15ull)));
+    }
+#pragma unroll
+    for (int d = 0; d < kHugeDepth; ++d) {
+      if (j - d < 0) break;  // wave-uniform
+      const uint32_t Rc = chv[d] >= c0 ? chunk_u(wv[d], (uint64_t)chv[d] << 4, a, b, T) : 0u;
+      S = mul_tab(A4, S) ^ Rc;
+    }
+  }
+  uint32_t t = gf_mul(S, cst[lane]);  // chunk position inside its round: x^(128 l)
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
+  return t;
+}
+
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
                                                           const uint32_t* __restrict__ crc_tab,
                                                           const uint32_t* __restrict__ consts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;       // [4][256] slice-by-4
-  uint32_t* A = lds + 1024;  // [4][256] (x) x^8192
-  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* tab = lds;           // [4][256] slice-by-4
+  uint32_t* A4 = lds + 1024;     // [4][256] (x) x^32768
+  uint32_t* cst = lds + 2048;    // [128] lane shifts x^(128 l), un-shifts x^(-8z), wave shifts x^(8192 w)
+  uint32_t* s_part = cst + 128;  // [4] wave sums
   const uint32_t ord_words = (sc.n_slots + 7u) / 8u * 4u;
-  const uint32_t wave_words = GORD ? 0u : ord_words + (sc.n_slots + 3u) / 4u * 4u;  // ord u16 + count u32
-  uint16_t* word = reinterpret_cast<uint16_t*>(lds + 2048 + wib * wave_words);
-  uint32_t* wcnt = lds + 2048 + wib * wave_words + ord_words;
-  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
+  uint16_t* word = reinterpret_cast<uint16_t*>(s_part + 4);
+  uint32_t* wcnt = s_part + 4 + ord_words;
+  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  for (uint32_t i = threadIdx.x; i < 1024u; i += kWaveBlock) {
+    tab[i] = crc_tab[i];
+    A4[i] = crc_tab[4096 + i];
+  }
+  for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
   const uint32_t nhuge = o.info[kInfoHuge];
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nhuge; i += gridDim.x * kWavesPerBlock) {
+  for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {  // workgroup-uniform
     const uint32_t r = o.big_list[B.n - 1u - i];
     RecView v = rec_view(B, r);
-    int64_t aux = 0;
-    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
-                           lane == 0};
-    if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
-    if (framed) {
-      const uint64_t D = v.e - v.st;
-      if (D >= 8) {
-        const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
-        if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
-        if (do_crc && D >= 12) {
-          const uint32_t c = crc_serial<1>(B.bytes, v.st, v.st + 8, T);
-          if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
-        }
-        if (do_crc && D >= 16) {
-          const uint64_t a = v.p0, b = v.e - 4;
-          const uint32_t c = b - a < 64 ? crc_serial<1>(B.bytes, a, b, T) : crc_wave(B.bytes, a, b, T, A, consts, lane);
+    const uint64_t D = v.e - v.st;
+    bool wide = false;  // payload CRC by the whole workgroup
+    uint64_t a = 0, b = 0;
+    if (framed && D >= 8) {
+      const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
+      if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
+      if (do_crc && D >= 12) {
+        const uint32_t c = crc_serial<1>(B.bytes, v.st, v.st + 8, T);
+        if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
+      }
+      if (do_crc && D >= 16) {
+        a = v.p0;
+        b = v.e - 4;
+        wide = b - a >= 64;
+        if (!wide) {
+          const uint32_t c = crc_serial<1>(B.bytes, a, b, T);
           if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
         }
       }
     }
-    for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
-    wave_lds_sync();
-    Src s;
-    s.init(B.bytes, v.p0, v.L);
-    int status = walk_example<COMPAT>(s, sink, aux);
-    if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-    wave_lds_sync();
-    wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
-    if (lane == 0) record_result(o, r, status, aux, v.verdict);
-    wave_lds_sync();
+    if (wide) {
+      uint32_t t = crc_huge_wave(B.bytes, a, b, T, A4, cst, wib, lane);
+      if (wib) t = gf_mul(t, cst[80 + wib]);
+      if (lane == 0) s_part[wib] = t;
+    }
+    __syncthreads();
+    if (wib == 0) {
+      if (wide) {
+        const uint64_t c1 = (b - 1) >> 4;
+        const uint32_t z = (uint32_t)(16ull * (c1 + 1ull) - b);  // zero bytes padding the last chunk
+        const uint32_t t = gf_mul(s_part[0] ^ s_part[1] ^ s_part[2] ^ s_part[3], cst[64 + z]);
+        if (crc_mask(~t) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
+      }
+      int64_t aux = 0;
+      CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
+                             lane == 0};
+      if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
+      for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
+      wave_lds_sync();
+      Src s;
+      s.init(B.bytes, v.p0, v.L);
+      int status = walk_example<COMPAT>(s, sink, aux);
+      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+      wave_lds_sync();
+      wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
+      if (lane == 0) record_result(o, r, status, aux, v.verdict);
+    }
+    __syncthreads();  // s_part and the dict are rewritten by the next record
   }
 }
 
@@ -2199,7 +2287,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   mark(kStageWaveCount);
   // staged (record span <= kWStage) and huge records: two launches, the second with a small LDS
   // footprint so the streaming CRC of huge records runs at full occupancy
-  const size_t huge_lds = 2048ull * 4 + kWavesPerBlock * ((S + 7) / 8 * 16 + (S + 3) / 4 * 16);
+  const size_t huge_fixed = (2048ull + 128 + 4) * 4;  // tables, constants, wave sums
+  const size_t huge_lds = huge_fixed + (S + 7) / 8 * 16 + S * 4;
+  const uint32_t huge_grid = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
   if (stage_lds_w <= kLdsBudget) {
     hipLaunchKernelGGL((k_stage_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_w, st, b,
                        sc, o, d_tab, d_consts);
@@ -2208,11 +2298,11 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        sc, o, d_tab, d_consts);
   }
   if (huge_lds <= kLdsBudget) {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), huge_lds, st, b, sc,
-                       o, d_tab, d_consts);
+    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(huge_grid), dim3(kWaveBlock), huge_lds, st, b, sc, o,
+                       d_tab, d_consts);
   } else {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), 2048ull * 4, st, b,
-                       sc, o, d_tab, d_consts);
+    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(huge_grid), dim3(kWaveBlock), huge_fixed, st, b, sc, o,
+                       d_tab, d_consts);
   }
   mark(kStageSpine);
   if (S > 0) hipLaunchKernelGGL(k_spine, dim3(S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
