@@ -216,7 +216,7 @@ def main() -> None:
     alg = {
         "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
         "k_slow_count": 0,
-        "k_wave_count": big_bytes + 16 * n_big,
+        "k_big_crc": big_bytes + 16 * n_big,
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         "k_list_gather": vals,

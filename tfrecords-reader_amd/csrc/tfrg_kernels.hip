@@ -804,6 +804,23 @@ struct FastSrc {
   }
   // as w4, any i (0 at and past L)
   __device__ __forceinline__ uint32_t w4s(uint32_t i) const { return i < L ? w4(i) : 0u; }
+  // 4 bytes at payload offset i, unmasked (the canonical walker bounds-checks what it uses)
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const { return lds_u32u(l, p + i); }
+};
+
+// The same payload view over HBM (records beyond the LDS stage): two aligned dword loads + a byte
+// funnel shift, clamped to the readable end of the batch (round_up(nbytes, 16)).
+struct FastSrcG {
+  const uint8_t* buf;
+  uint64_t base;  // absolute payload start
+  uint32_t L;
+  uint64_t lim;   // last readable dword
+  __device__ __forceinline__ uint32_t u32(uint32_t i) const {
+    const uint64_t a = base + i, a0 = a & ~3ull;
+    const uint32_t w0 = *reinterpret_cast<const uint32_t*>(buf + (a0 < lim ? a0 : lim));
+    const uint32_t w1 = *reinterpret_cast<const uint32_t*>(buf + (a0 + 4 < lim ? a0 + 4 : lim));
+    return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(a & 3u));
+  }
 };
 
 // varint of <= 4 bytes (values < 2^28: identical in compat and spec mode); false = bail
@@ -858,10 +875,11 @@ __device__ __forceinline__ bool ffield(const FastSrc& s, uint32_t& pos, uint32_t
 
 // number of varints in a packed chunk [o, e) that ends on a terminator, with no varint longer
 // than 10 bytes (else bail: 'Too many bytes' / overrun semantics are the exact walker's)
-__device__ __forceinline__ bool count_packed(const FastSrc& s, uint32_t o, uint32_t e, uint32_t& cnt) {
+template <class S>
+__device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e, uint32_t& cnt) {
   uint32_t run = 0, terms = 0, last = 0x80u;
   for (uint32_t i = o; i < e; i += 4) {
-    const uint32_t w = lds_u32u(s.l, s.p + i);
+    const uint32_t w = s.u32(i);
     const uint32_t rem = e - i;
     const uint32_t valid = rem >= 4 ? 0x80808080u : (0x80808080u & ((1u << (8 * rem)) - 1u));
     const uint32_t term = ~w & valid;
@@ -908,22 +926,35 @@ struct LdsKeys {
   const uint32_t* ht;    // [mask+1] key id + 1
   const uint32_t* rec;   // [n_keys][kKrWords]
   uint32_t mask;
+  const uint8_t* blob = nullptr;   // global key bytes + offsets: the middle of keys longer than 8 bytes
+  const uint32_t* koff = nullptr;
 };
 
 // key id for key bytes at [ko, ko+kl) of the payload; -1 = not a plain hit (bail)
-__device__ __forceinline__ int fast_lookup(const FastSrc& s, const LdsKeys& K, uint32_t ko, uint32_t kl) {
-  if (kl > 8u) return -1;  // longer keys: exact walker (byte compare)
-  uint32_t w0 = lds_u32u(s.l, s.p + ko);
+template <class S>
+__device__ __forceinline__ int fast_lookup(const S& s, const LdsKeys& K, uint32_t ko, uint32_t kl) {
+  if (kl > 256u) return -1;  // very long keys: exact walker
+  uint32_t w0 = s.u32(ko);
   if (kl < 4) w0 &= (1u << (8 * kl)) - 1u;
-  const uint32_t w1 = kl > 4 ? lds_u32u(s.l, s.p + ko + kl - 4) : 0u;
+  const uint32_t w1 = kl > 4 ? s.u32(ko + kl - 4) : 0u;
   const uint32_t h = key_hash_words(kl, w0, w1);
   uint32_t j = h & K.mask;
   for (uint32_t probe = 0; probe <= K.mask; ++probe) {
     const uint32_t e = K.ht[j];
     if (!e) return -1;
     const uint32_t* r = K.rec + (e - 1) * kKrWords;
-    if (r[kKrHash] == h && r[kKrLen] == kl && r[kKrW0] == w0 && r[kKrW1] == w1)
-      return (r[kKrFlags] & 1u) ? -1 : (int)(e - 1);
+    if (r[kKrHash] == h && r[kKrLen] == kl && r[kKrW0] == w0 && r[kKrW1] == w1) {
+      // (length, first 4, last 4) identify keys of <= 8 bytes; longer ones compare the middle too
+      bool eq = true;
+      if (kl > 8u) {
+        const uint8_t* kb = K.blob + K.koff[e - 1];
+        for (uint32_t i = 4; eq && i < kl - 4u; i += 4) {
+          const uint32_t jj = i + 4u <= kl - 4u ? i : kl - 8u;
+          eq = s.u32(ko + jj) == load_u32_unaligned(kb, jj);
+        }
+      }
+      if (eq) return (r[kKrFlags] & 1u) ? -1 : (int)(e - 1);
+    }
     j = (j + 1) & K.mask;
   }
   return -1;
@@ -1001,10 +1032,11 @@ __device__ __forceinline__ bool fast_single(const FastSrc& s, uint32_t kind, uin
 // type 2, 1..3-byte length, body inside `end`. Anything else is not canonical (ok = false); the
 // outputs are then garbage but positions stay inside the record, so the caller may keep computing
 // and decide once.
-__device__ __forceinline__ bool hdr2(const FastSrc& s, uint32_t pos, uint32_t end, uint32_t& fn, uint32_t& off,
+template <class S>
+__device__ __forceinline__ bool hdr2(const S& s, uint32_t pos, uint32_t end, uint32_t& fn, uint32_t& off,
                                      uint32_t& len) {
   pos = pos < s.L ? pos : s.L;
-  const uint32_t w = lds_u32u(s.l, s.p + pos);
+  const uint32_t w = s.u32(pos);
   const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
   const uint32_t c1 = b1 >> 7, c12 = c1 & (b2 >> 7);
   uint32_t l = b1 & 0x7fu;
@@ -1019,8 +1051,8 @@ __device__ __forceinline__ bool hdr2(const FastSrc& s, uint32_t pos, uint32_t en
 // Returns TFRG_OK with the dict in sink.ord / cnt (or count) / loc, or kBail (exact walker).
 // Every level is a single canonical pass: one Features field spanning the Example, map entries of
 // exactly (key #1, value #2), one kind field spanning the Feature, list chunks of field #1.
-template <bool COMPAT, class Sink>
-__device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Sink& sink) {
+template <bool COMPAT, class Sink, class S>
+__device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sink) {
   const uint32_t L = s.L;
   uint32_t fn, fo, fl;
   bool ok = hdr2(s, 0, L, fn, fo, fl) & (fn == 1u) & (fo + fl == L);
@@ -1085,10 +1117,10 @@ __device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Sin
         lv = make_uint2((uint32_t)(s.base + c0o), c0l);
         cw = 1u | kCountInline;
       } else if (kind == TFRG_KIND_FLOAT) {
-        lv = make_uint2(lds_u32u(s.l, s.p + c0o), 0u);
+        lv = make_uint2(s.u32(c0o), 0u);
         cw = 1u | kCountInline;
       } else if (c0l <= 4u) {  // one varint of <= 4 bytes: value < 2^28, same in both varint modes
-        const uint32_t w = lds_u32u(s.l, s.p + c0o);
+        const uint32_t w = s.u32(c0o);
         const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
         lv = make_uint2(x & ((1u << (7u * c0l)) - 1u), 0u);
         cw = 1u | kCountInline;
@@ -1106,9 +1138,10 @@ __device__ __forceinline__ int fast_walk(const FastSrc& s, const LdsKeys& K, Sin
 // Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
 // bytes and of the payload (the TFRecord spec; absent from the reference), from the
 // wave's LDS stage (STAGED) or from HBM.
+// payload_crc = false leaves the payload CRC of a record above lane_max to k_wave_count.
 template <int R, bool STAGED>
 __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, const LdsTab<R>& T, const uint8_t* stage,
-                                               uint64_t lo16) {
+                                               uint64_t lo16, bool payload_crc = true) {
   if (B.flags & kFlagPayloadOnly) return;
   const bool do_crc = !(B.flags & kFlagNoCrc);
   const uint64_t D = v.e - v.st;
@@ -1132,7 +1165,7 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
     }
     if (crc_mask(c) == stored) v.verdict |= TFRG_V_LEN_CRC;
   }
-  if (do_crc && D >= 16) {
+  if (do_crc && payload_crc && D >= 16) {
     uint32_t c, stored;
     if constexpr (STAGED) {
       c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
@@ -1181,7 +1214,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
   }
   __syncthreads();
-  const LdsKeys K{kht, krec, sc.ht_mask};
+  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
 
   for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
@@ -1225,8 +1258,19 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
       done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
     }
-    // everything else of this wave's lane records goes to the exact walker
-    const bool slow = mine && !done;
+    // records above lane_max: the canonical walk straight from HBM, one record per lane (64 latency
+    // chains in flight per wave); their payload CRC is k_wave_count's streaming pass
+    const bool bigw = fast_ok && valid && !mine;
+    if (__ballot(bigw)) {
+      if (bigw) {
+        frame_verdicts<R, false>(B, v, T, nullptr, 0, false);
+        for (uint32_t k = 0; k < S; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+        const FastSrcG fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
+        done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+      }
+    }
+    // everything else of this wave's records goes to the exact walker
+    const bool slow = valid && !done;
     const uint64_t sm = __ballot(slow);
     if (sm) {
       uint32_t b0 = 0;
@@ -1262,7 +1306,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
 // record of the slow list, reading the record from HBM; also the framing errors and schema misses.
 template <int R, bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab) {
+                                                           const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t nslow = o.info[kInfoSlow];
   if (blockIdx.x * kLaneBlock >= nslow) return;  // block-uniform
@@ -1282,7 +1326,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema
     if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
     int status = v.status;
     if (status == TFRG_OK) {
-      frame_verdicts<R, false>(B, v, T, nullptr, 0);
+      frame_verdicts<R, false>(B, v, T, nullptr, 0, v.e - v.st <= lane_max);  // larger: k_wave_count
       sink.reset();
       Src s;
       s.init(B.bytes, v.p0, v.L);
@@ -1471,19 +1515,19 @@ __device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a
   return t;
 }
 
-template <bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema sc, DevOut o,
-                                                          const uint32_t* __restrict__ crc_tab,
-                                                          const uint32_t* __restrict__ consts) {
+// Payload CRC-32C of every record above lane_max (their framing bits and walk are the lane / slow
+// kernels'): one workgroup per record, the DATA_CRC verdict bit OR-ed into the verdict column.
+__global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, const uint32_t* __restrict__ crc_tab,
+                                                       const uint32_t* __restrict__ consts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;           // [4][256] slice-by-4
   uint32_t* A4 = lds + 1024;     // [4][256] (x) x^32768
   uint32_t* cst = lds + 2048;    // [128] lane shifts x^(128 l), un-shifts x^(-8z), wave shifts x^(8192 w)
   uint32_t* s_part = cst + 128;  // [4] wave sums
-  const uint32_t ord_words = (sc.n_slots + 7u) / 8u * 4u;
-  uint16_t* word = reinterpret_cast<uint16_t*>(s_part + 4);
-  uint32_t* wcnt = s_part + 4 + ord_words;
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t nbig = o.info[kInfoBig], nhuge = o.info[kInfoHuge];
+  if (B.flags & (kFlagPayloadOnly | kFlagNoCrc)) return;
+  if (blockIdx.x >= nbig + nhuge) return;  // workgroup-uniform
   for (uint32_t i = threadIdx.x; i < 1024u; i += kWaveBlock) {
     tab[i] = crc_tab[i];
     A4[i] = crc_tab[4096 + i];
@@ -1491,60 +1535,28 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_count(DevBatch B, DevSchema
   for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  const uint32_t nhuge = o.info[kInfoHuge];
-  const bool framed = !(B.flags & kFlagPayloadOnly);
-  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-  for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {  // workgroup-uniform
-    const uint32_t r = o.big_list[B.n - 1u - i];
-    RecView v = rec_view(B, r);
-    const uint64_t D = v.e - v.st;
-    bool wide = false;  // payload CRC by the whole workgroup
-    uint64_t a = 0, b = 0;
-    if (framed && D >= 8) {
-      const uint64_t lenf = load_u64_unaligned(B.bytes, v.st);
-      if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
-      if (do_crc && D >= 12) {
-        const uint32_t c = crc_serial<1>(B.bytes, v.st, v.st + 8, T);
-        if (crc_mask(c) == load_u32_unaligned(B.bytes, v.st + 8)) v.verdict |= TFRG_V_LEN_CRC;
-      }
-      if (do_crc && D >= 16) {
-        a = v.p0;
-        b = v.e - 4;
-        wide = b - a >= 64;
-        if (!wide) {
-          const uint32_t c = crc_serial<1>(B.bytes, a, b, T);
-          if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
-        }
-      }
-    }
-    if (wide) {
+  for (uint32_t i = blockIdx.x; i < nbig + nhuge; i += gridDim.x) {  // workgroup-uniform
+    PHASE_MARK(h0);
+    const uint32_t r = i < nbig ? o.big_list[i] : o.big_list[B.n - 1u - (i - nbig)];
+    const RecView v = rec_view(B, r);
+    if (v.e - v.st < 16) continue;  // no payload CRC (lane_max below the framing size)
+    const uint64_t a = v.p0, b = v.e - 4;
+    uint32_t c;
+    if (b - a >= 64) {
       uint32_t t = crc_huge_wave(B.bytes, a, b, T, A4, cst, wib, lane);
       if (wib) t = gf_mul(t, cst[80 + wib]);
       if (lane == 0) s_part[wib] = t;
+      __syncthreads();
+      const uint64_t c1 = (b - 1) >> 4;
+      const uint32_t z = (uint32_t)(16ull * (c1 + 1ull) - b);  // zero bytes padding the last chunk
+      c = ~gf_mul(s_part[0] ^ s_part[1] ^ s_part[2] ^ s_part[3], cst[64 + z]);
+      __syncthreads();  // s_part is rewritten by the next record
+    } else {
+      c = crc_serial<1>(B.bytes, a, b, T);
     }
-    __syncthreads();
-    if (wib == 0) {
-      if (wide) {
-        const uint64_t c1 = (b - 1) >> 4;
-        const uint32_t z = (uint32_t)(16ull * (c1 + 1ull) - b);  // zero bytes padding the last chunk
-        const uint32_t t = gf_mul(s_part[0] ^ s_part[1] ^ s_part[2] ^ s_part[3], cst[64 + z]);
-        if (crc_mask(~t) == load_u32_unaligned(B.bytes, b)) v.verdict |= TFRG_V_DATA_CRC;
-      }
-      int64_t aux = 0;
-      CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
-                             lane == 0};
-      if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
-      for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
-      wave_lds_sync();
-      Src s;
-      s.init(B.bytes, v.p0, v.L);
-      int status = walk_example<COMPAT>(s, sink, aux);
-      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-      wave_lds_sync();
-      wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
-      if (lane == 0) record_result(o, r, status, aux, v.verdict);
-    }
-    __syncthreads();  // s_part and the dict are rewritten by the next record
+    if (threadIdx.x == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
+    PHASE_MARK(h1);
+    if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
   }
 }
 
@@ -1638,7 +1650,7 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchem
   }
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  const LdsKeys K{kht, krec, sc.ht_mask};
+  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const uint32_t nbig = o.info[kInfoBig];
   const bool framed = !(B.flags & kFlagPayloadOnly);
   const bool do_crc = framed && !(B.flags & kFlagNoCrc);
@@ -2093,7 +2105,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchem
     const RecView v = rec_view(B, r);
     for (uint32_t k = lane; k < sc.n_slots; k += 64) {
       const size_t at = (size_t)k * B.n + r;
-      if (!o.order[at]) continue;
+      const uint32_t c = o.count[at];
+      if (!c || (c & kCountInline)) continue;  // absent / empty, or written inline by k_down_gather
       const uint2 lc = o.loc[at];
       const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
       Src s;
@@ -2181,7 +2194,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
     uint64_t dst = 0;
     if (ok && lane < sc.n_slots) {
       const size_t at = (size_t)lane * B.n + r;
-      present = o.order[at] != 0;
+      const uint32_t c = o.count[at];
+      present = c && !(c & kCountInline);  // inline single values are k_down_gather's
       lc = o.loc[at];
       dst = o.slot_base[lane] + o.rs[(size_t)lane * (B.n + 1) + r];
       kind = sc.slot_kind[lane];
@@ -2209,7 +2223,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
       uint64_t dk = 0;
       if (k < sc.n_slots) {
         const size_t at = (size_t)k * B.n + r;
-        pk = o.order[at] != 0;
+        const uint32_t c = o.count[at];
+        pk = c && !(c & kCountInline);
         lk = o.loc[at];
         dk = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
         kk = sc.slot_kind[k];
@@ -2227,10 +2242,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (slice-by-8: 8 KiB per copy)
 
-constexpr size_t kLdsBudget = 128 * 1024;     // wavefront kernels: above this the dict goes to the columns
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_slow_count",  "k_wave_count", "k_spine",
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_slow_count",  "k_big_crc",    "k_spine",
                                              "k_down_gather", "k_list_gather", "k_wave_gather"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2253,8 +2267,6 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t wave_shared = (2048ull + 128 + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
   const size_t wave_per = (size_t)kWStageStride + kMaxEnt * 4 + kLdsMaxKeys * 4;
   const size_t dict_wave = r16(S * 2) + r16(S * 4);
-  const size_t stage_lds_w = wave_shared + kWavesPerBlock * (wave_per + dict_wave);
-  const size_t stage_lds_wg = wave_shared + kWavesPerBlock * wave_per;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
 
   mark(kStageLaneCount);
@@ -2279,30 +2291,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   mark(kStageSlowCount);
   if (slow_lds <= kLaneLdsBudget) {
     hipLaunchKernelGGL((k_slow_count<1, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), slow_lds, st, b, sc,
-                       o, d_tab);
+                       o, d_tab, cfg.lane_max);
   } else {
     hipLaunchKernelGGL((k_slow_count<1, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), 2048ull * 4, st, b,
-                       sc, o, d_tab);
+                       sc, o, d_tab, cfg.lane_max);
   }
   mark(kStageWaveCount);
-  // staged (record span <= kWStage) and huge records: two launches, the second with a small LDS
-  // footprint so the streaming CRC of huge records runs at full occupancy
-  const size_t huge_fixed = (2048ull + 128 + 4) * 4;  // tables, constants, wave sums
-  const size_t huge_lds = huge_fixed + (S + 7) / 8 * 16 + S * 4;
-  const uint32_t huge_grid = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
-  if (stage_lds_w <= kLdsBudget) {
-    hipLaunchKernelGGL((k_stage_count<COMPAT, false>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_w, st, b,
-                       sc, o, d_tab, d_consts);
-  } else {
-    hipLaunchKernelGGL((k_stage_count<COMPAT, true>), dim3(cfg.wave_grid), dim3(kWaveBlock), stage_lds_wg, st, b,
-                       sc, o, d_tab, d_consts);
-  }
-  if (huge_lds <= kLdsBudget) {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, false>), dim3(huge_grid), dim3(kWaveBlock), huge_lds, st, b, sc, o,
-                       d_tab, d_consts);
-  } else {
-    hipLaunchKernelGGL((k_wave_count<COMPAT, true>), dim3(huge_grid), dim3(kWaveBlock), huge_fixed, st, b, sc, o,
-                       d_tab, d_consts);
+  {
+    const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
+    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (2048 + 128 + 4) * 4, st, b, o, d_tab, d_consts);
   }
   mark(kStageSpine);
   if (S > 0) hipLaunchKernelGGL(k_spine, dim3(S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);

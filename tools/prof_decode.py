@@ -68,7 +68,7 @@ def main():
         arr = (ctypes.c_ulonglong * 16)()
         L.tfrg_debug_phase(arr, 16, 1)
         names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
-                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane"]
+                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane", "h.crc", "h.walk"]
         tot = arr[7] or 1
         for i, nm in enumerate(names):
             print(f"{nm:10s} {arr[i]:>16d} {arr[i] / tot:8.3f}")
