@@ -1449,13 +1449,16 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
   }
 }
 
+#ifndef TFRG_HUGE_DEPTH
+#define TFRG_HUGE_DEPTH 8
+#endif
 // Huge records (span beyond the LDS stage): one WORKGROUP per record. The payload CRC is split over
 // the 4 waves by interleaved 1 KiB rounds (64 lanes x 16-byte chunks, rounds counted from the end;
 // wave w takes rounds w, w+4, w+8, ...) with kHugeDepth rounds of loads in flight per lane. A lane's
 // state advances by x^32768 per step of its wave (A4 tables), wave w's lane-combined sum is shifted
 // by x^(8192 w), and the four sums XOR together (crc32c.h algebra). Wave 0 then runs the exact,
 // wave-uniform walk over the (now L2-warm) record.
-constexpr int kHugeDepth = 4;
+constexpr int kHugeDepth = TFRG_HUGE_DEPTH;
 
 // U(0, 16-byte chunk at q) of the payload [a, b): bytes outside zeroed, the first 4 payload bytes
 // inverted (the ~0 initial state)
@@ -1535,11 +1538,19 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
   for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  for (uint32_t i = blockIdx.x; i < nbig + nhuge; i += gridDim.x) {  // workgroup-uniform
+  __shared__ uint32_t s_next;
+  for (uint32_t i = blockIdx.x;;) {  // records taken dynamically (skewed sizes), workgroup-uniform
+    if (i >= nbig + nhuge) break;
     PHASE_MARK(h0);
     const uint32_t r = i < nbig ? o.big_list[i] : o.big_list[B.n - 1u - (i - nbig)];
+    if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(&o.info[kInfoCrcNext], 1u);
     const RecView v = rec_view(B, r);
-    if (v.e - v.st < 16) continue;  // no payload CRC (lane_max below the framing size)
+    if (v.e - v.st < 16) {  // no payload CRC (lane_max below the framing size)
+      __syncthreads();
+      i = s_next;
+      __syncthreads();
+      continue;
+    }
     const uint64_t a = v.p0, b = v.e - 4;
     uint32_t c;
     if (b - a >= 64) {
@@ -1557,6 +1568,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     if (threadIdx.x == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
     PHASE_MARK(h1);
     if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
+    __syncthreads();
+    i = s_next;
+    __syncthreads();  // s_next is rewritten by the next record
   }
 }
 
