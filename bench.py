@@ -277,6 +277,15 @@ def main() -> None:
     sb_ms = float(np.median(sb_ms))
     sb_bytes = int((sb_en - sb_st).sum())
 
+    # HBM bytes per launch of the dominant kernel from the committed PMC passes of this workload
+    # (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM); null if none
+    traffic, traffic_src = None, None
+    tf = REPO / "profiles" / f"traffic_{args.config}.json"
+    if tf.is_file():
+        t = json.loads(tf.read_text())
+        if dominant in t.get("kernel", "") and args.files is None:
+            traffic, traffic_src = int(t["traffic_bytes"]), f"profiles/{tf.name}"
+
     ms_step = elapsed / args.steps * 1e3
     gib_s_rank = framed_bytes / (ms_step / 1e3) / 2**30
     value = framed_bytes * world / (elapsed / args.steps) / 2**30
@@ -319,7 +328,8 @@ def main() -> None:
                 "peak": PEAK_HBM_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "algorithmic_bytes_per_launch": a_bytes,
                 "achievable_read_GBps": round(hbm_read_gbs, 1),
             },

@@ -59,7 +59,6 @@ enum InfoIdx : uint32_t {
   kInfoSlow = 7,         // lane records left to the exact (slow) walker
   kInfoSpineDone = 8,    // spine workgroups finished (the last one computes the column bases)
   kInfoNeed = 9,         // lane records with an out-of-line list (k_list_gather; listed in slow_list)
-  kInfoCrcNext = 10,     // k_big_crc's dynamic record counter
   kInfoCount = 16
 };
 

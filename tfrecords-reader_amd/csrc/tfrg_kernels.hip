@@ -1,23 +1,23 @@
 // tfrg_kernels.hip — gfx950 kernels for the TFRecord -> tf.train.Example -> Feature path.
 //
-// Pipeline for one batch of framed records resident in HBM (launch_decode):
-//   1. k_lane_count  : one LANE per record (records <= lane_max bytes). Framing check, masked
-//                      CRC-32C of length and payload (slice-by-4, bank-replicated LDS tables),
-//                      then a reference-exact walk of Example -> Features -> map entries ->
-//                      Feature -> value list (decoder.pyx:53-300) that validates every level in
-//                      the reference's error precedence and records, per (key, kind) slot, the
-//                      value count, the list location and the key's dict position.
-//                      Larger records are appended to a work list.
-//   2. k_wave_count  : one WAVEFRONT per large record: the CRC is split over 64 lanes in 16-byte
-//                      chunks (coalesced 1 KiB rounds) and recombined with GF(2) shift operators;
-//                      the structure walk runs wave-uniform.
-//   3. k_scan_*      : per-slot exclusive scan of the counts (reduce -> spine -> downsweep;
-//                      no inter-workgroup waiting).
-//   4. k_base        : per-kind column bases.
-//   5. k_lane_gather / k_wave_gather : write the int64 / float / bytes-view values of every
-//                      present slot into per-slot contiguous columns.
+// Pipeline for one batch of framed records resident in HBM (launch_decode; DESIGN.md §Kernels):
+//   1. k_lane_count  : one LANE per record. Records <= lane_max: the wave's contiguous span staged
+//                      in LDS, framing check, masked CRC-32C of length and payload (slice-by-4 LDS
+//                      tables), single-pass canonical walk of Example -> Features -> map entries ->
+//                      Feature -> list (decoder.pyx:53-300 on canonical input). Records above
+//                      lane_max: the same walk straight from HBM (their payload CRC is step 3).
+//                      Per-slot counts summed per 256-record tile. Everything else -> slow list.
+//   2. k_slow_count  : the exact reference walk (level-by-level error precedence, dict semantics,
+//                      schema misses) for the slow list, one lane per record.
+//   3. k_big_crc     : payload CRC of records above lane_max, one workgroup per record, the four
+//                      waves recombined with GF(2) shift operators (crc32c.h).
+//   4. k_spine       : per-slot exclusive scan of the tile sums + per-kind column bases.
+//   5. k_down_gather : row splits (tile prefix + in-tile scan) and inline single values.
+//   6. k_list_gather / k_stage_gather / k_wave_gather : out-of-line lists of lane records and of
+//                      records above lane_max.
 //
-// All walks share one templated walker so the lane and wave paths cannot drift apart.
+// The canonical walker and the exact walker share the count/gather sinks, so both paths produce
+// identical columns (tests/test_gpu_parity.py forces each path on the same inputs).
 #include <hip/hip_runtime.h>
 #include <type_traits>
 #include "tfrg_internal.h"
@@ -523,52 +523,6 @@ __device__ __forceinline__ uint64_t load_u64_unaligned(const uint8_t* buf, uint6
   return (uint64_t)load_u32_unaligned(buf, a) | ((uint64_t)load_u32_unaligned(buf, a + 4) << 32);
 }
 
-// Wavefront CRC-32C of absolute bytes [a, b), b - a >= 64. Chunks are the buffer's aligned
-// 16-byte blocks; rounds of 64 chunks are taken from the END so that lane l's chunk in the last
-// round is followed by exactly l chunks. Each lane keeps S_l <- S_l (x) x^8192 ^ U(0, chunk); the
-// payload is then  xor_l S_l (x) x^(128 l), un-shifted by the z zero bytes padding the last chunk.
-// Leading bytes before a are zero (free for a zero initial state); the first 4 payload bytes are
-// inverted (the ~0 initial state).
-__device__ uint32_t crc_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
-                             const uint32_t* A /* LDS [4][256]: (x) x^8192 */, const uint32_t* consts,
-                             uint32_t lane) {
-  const uint64_t c0 = a >> 4, c1 = (b - 1) >> 4;
-  const uint64_t nch = c1 - c0 + 1;
-  const int64_t rounds = (int64_t)((nch + 63) >> 6);
-  uint32_t S = 0;
-  for (int64_t k = rounds - 1; k >= 0; --k) {
-    const int64_t ch = (int64_t)c1 - 64 * k - (int64_t)lane;
-    uint32_t Rc = 0;
-    if (ch >= (int64_t)c0) {
-      const uint64_t q = (uint64_t)ch << 4;
-      const uint4 w = *reinterpret_cast<const uint4*>(buf + q);
-      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-      if (q < a + 4 || q + 16 > b) {  // edge chunk: mask outside bytes, invert the first 4
-#pragma unroll
-        for (int k2 = 0; k2 < 4; ++k2) {
-          uint32_t keep = 0, inv = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint64_t ba = q + 4ull * k2 + j;
-            if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
-            if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
-          }
-          ws[k2] = (ws[k2] & keep) ^ inv;
-        }
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
-    }
-    S = A[S & 0xffu] ^ A[256 + ((S >> 8) & 0xffu)] ^ A[512 + ((S >> 16) & 0xffu)] ^ A[768 + (S >> 24)] ^ Rc;
-  }
-  uint32_t t = gf_mul(S, consts[lane]);
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
-  const uint32_t z = (uint32_t)(16 * (c1 + 1) - b);
-  t = gf_mul(t, consts[64 + z]);
-  return ~t;
-}
-
 // ------------------------------------------------------------------------------------------------
 // Per-record framing: payload range, verdict bits, read errors.
 // ------------------------------------------------------------------------------------------------
@@ -693,7 +647,6 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave (wavefront kernels)
 constexpr uint32_t kWStageStride = kWStage + 64;
-constexpr uint32_t kMaxEnt = 256;                   // map entries per record on the parallel path
 
 // copy absolute bytes [lo16, hi) (lo16 16-aligned) into dst
 __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
@@ -1339,53 +1292,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema
 }
 
 // ------------------------------------------------------------------------------------------------
-// Wavefront-per-record kernels for records above lane_max. A record that fits kWStage is staged
-// into the wave's LDS (coalesced 16 B loads), CRC'd from LDS by all 64 lanes, and walked in two
-// phases: the Features level is walked once (wave-uniform) to list the map entries, then each
-// lane parses its own entries (key lookup, Feature, list validation + count) — the per-entry work
-// that dominates wide schemas runs 64-wide. Anything non-canonical falls back to the exact walker.
-// Larger records keep the streaming CRC and the wave-uniform exact walk from HBM.
+// Records above lane_max: payload CRC (k_big_crc) and the helpers of their wavefront gathers.
 // ------------------------------------------------------------------------------------------------
-
-// wave CRC-32C of stage bytes [a, b) (stage offsets, a/b arbitrary), same algebra as crc_wave
-__device__ uint32_t crc_wave_lds(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<1>& T, const uint32_t* A,
-                                 const uint32_t* consts, uint32_t lane) {
-  const uint32_t c0 = a >> 4, c1 = (b - 1) >> 4;
-  const uint32_t nch = c1 - c0 + 1;
-  const int32_t rounds = (int32_t)((nch + 63) >> 6);
-  uint32_t S = 0;
-  for (int32_t k = rounds - 1; k >= 0; --k) {
-    const int32_t ch = (int32_t)c1 - 64 * k - (int32_t)lane;
-    uint32_t Rc = 0;
-    if (ch >= (int32_t)c0) {
-      const uint32_t q = (uint32_t)ch << 4;
-      const uint4 w = *reinterpret_cast<const uint4*>(l + q);
-      uint32_t ws[4] = {w.x, w.y, w.z, w.w};
-      if (q < a + 4 || q + 16 > b) {
-#pragma unroll
-        for (int k2 = 0; k2 < 4; ++k2) {
-          uint32_t keep = 0, inv = 0;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const uint32_t ba = q + 4u * k2 + j;
-            if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
-            if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
-          }
-          ws[k2] = (ws[k2] & keep) ^ inv;
-        }
-      }
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
-    }
-    S = A[S & 0xffu] ^ A[256 + ((S >> 8) & 0xffu)] ^ A[512 + ((S >> 16) & 0xffu)] ^ A[768 + (S >> 24)] ^ Rc;
-  }
-  uint32_t t = gf_mul(S, consts[lane]);
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
-  const uint32_t z = 16u * (c1 + 1) - b;
-  t = gf_mul(t, consts[64 + z]);
-  return ~t;
-}
 
 // Scalar read of a canonical length-delimited field-1 header at `q`: tag 0x0a + length varint of
 // <= 3 bytes; sets the body offset/length (body inside the payload) or returns false (bail).
@@ -1410,23 +1318,6 @@ __device__ __forceinline__ bool hdr_0a(const FastSrc& s, uint32_t q, uint32_t& b
   bo = q + h;
   bl = len;
   return bo <= s.L && len <= s.L - bo;
-}
-
-// Phase B of the parallel walk for one entry: fills slot/rank-free results; false = bail.
-__device__ __forceinline__ bool entry_fast(const FastSrc& s, const LdsKeys& K, uint32_t eo, uint32_t el, int& kid,
-                                           int& slot, uint32_t& lo, uint32_t& ll, uint32_t& cnt) {
-  uint32_t e = eo;
-  const uint32_t ee = eo + el;
-  uint32_t kn, ko, kl, vn, vo, vl, kind, g;
-  if (!ffield(s, e, ee, kn, ko, kl) || kn != 1u) return false;
-  if (!ffield(s, e, ee, vn, vo, vl) || vn != 2u || e != ee) return false;
-  kid = fast_lookup(s, K, ko, kl);
-  if (kid < 0) return false;
-  g = vo;
-  if (!ffield(s, g, vo + vl, kind, lo, ll) || g != vo + vl || kind < 1u || kind > 3u) return false;
-  if (!fast_list_count(s, kind, lo, ll, cnt)) return false;
-  slot = (int)K.rec[(uint32_t)kid * kKrWords + kKrSlot1 + kind - 1];
-  return slot >= 0;
 }
 
 // Finalize of a wavefront record: order/count columns and tile sums, one slot per lane. Counts come
@@ -1487,18 +1378,17 @@ __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
   return M[S & 0xffu] ^ M[256 + ((S >> 8) & 0xffu)] ^ M[512 + ((S >> 16) & 0xffu)] ^ M[768 + (S >> 24)];
 }
 
-// this wave's share of U(0, payload') over [a, b) (b - a >= 64), lane-combined, not yet shifted
-__device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
-                                                  const uint32_t* A4, const uint32_t* cst, uint32_t w, uint32_t lane) {
-  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
-  const int64_t rounds = (c1 - c0 + 64) >> 6;
-  const int64_t J = rounds > (int64_t)w ? (rounds - (int64_t)w + 3) / 4 : 0;  // rounds w + 4j, j < J
+// Horner over this wave's rounds j = J-1 .. 0, DEPTH rounds of loads in flight
+template <int DEPTH>
+__device__ __forceinline__ uint32_t crc_rounds(const uint8_t* buf, uint64_t a, uint64_t b, int64_t c0, int64_t c1,
+                                               int64_t J, const LdsTab<1>& T, const uint32_t* A4, uint32_t w,
+                                               uint32_t lane) {
   uint32_t S = 0;
-  for (int64_t j = J - 1; j >= 0; j -= kHugeDepth) {  // Horner from the payload start (largest round)
-    uint4 wv[kHugeDepth];
-    int64_t chv[kHugeDepth];
+  for (int64_t j = J - 1; j >= 0; j -= DEPTH) {  // from the payload start (largest round)
+    uint4 wv[DEPTH];
+    int64_t chv[DEPTH];
 #pragma unroll
-    for (int d = 0; d < kHugeDepth; ++d) {  // every load of the group in flight before any use
+    for (int d = 0; d < DEPTH; ++d) {  // every load of the group in flight before any use
       const int64_t k = (int64_t)w + 4 * (j - d);
       const int64_t ch = c1 - 64 * k - (int64_t)lane;
       chv[d] = ch;
@@ -1506,12 +1396,23 @@ __device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a
       wv[d] = *reinterpret_cast<const uint4*>(buf + (in ? (uint64_t)ch << 4 : (a & ~15ull)));
     }
 #pragma unroll
-    for (int d = 0; d < kHugeDepth; ++d) {
+    for (int d = 0; d < DEPTH; ++d) {
       if (j - d < 0) break;  // wave-uniform
       const uint32_t Rc = chv[d] >= c0 ? chunk_u(wv[d], (uint64_t)chv[d] << 4, a, b, T) : 0u;
       S = mul_tab(A4, S) ^ Rc;
     }
   }
+  return S;
+}
+
+// this wave's share of U(0, payload') over [a, b) (b - a >= 64), lane-combined, not yet shifted
+__device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
+                                                  const uint32_t* A4, const uint32_t* cst, uint32_t w, uint32_t lane) {
+  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
+  const int64_t rounds = (c1 - c0 + 64) >> 6;
+  const int64_t J = rounds > (int64_t)w ? (rounds - (int64_t)w + 3) / 4 : 0;  // rounds w + 4j, j < J
+  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth>(buf, a, b, c0, c1, J, T, A4, w, lane)
+                                     : crc_rounds<2>(buf, a, b, c0, c1, J, T, A4, w, lane);
   uint32_t t = gf_mul(S, cst[lane]);  // chunk position inside its round: x^(128 l)
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
@@ -1538,19 +1439,11 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
   for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  __shared__ uint32_t s_next;
-  for (uint32_t i = blockIdx.x;;) {  // records taken dynamically (skewed sizes), workgroup-uniform
-    if (i >= nbig + nhuge) break;
+  for (uint32_t i = blockIdx.x; i < nbig + nhuge; i += gridDim.x) {  // workgroup-uniform
     PHASE_MARK(h0);
     const uint32_t r = i < nbig ? o.big_list[i] : o.big_list[B.n - 1u - (i - nbig)];
-    if (threadIdx.x == 0) s_next = gridDim.x + atomicAdd(&o.info[kInfoCrcNext], 1u);
     const RecView v = rec_view(B, r);
-    if (v.e - v.st < 16) {  // no payload CRC (lane_max below the framing size)
-      __syncthreads();
-      i = s_next;
-      __syncthreads();
-      continue;
-    }
+    if (v.e - v.st < 16) continue;  // no payload CRC (lane_max below the framing size)
     const uint64_t a = v.p0, b = v.e - 4;
     uint32_t c;
     if (b - a >= 64) {
@@ -1568,9 +1461,6 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     if (threadIdx.x == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
     PHASE_MARK(h1);
     if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
-    __syncthreads();
-    i = s_next;
-    __syncthreads();  // s_next is rewritten by the next record
   }
 }
 
@@ -1631,164 +1521,6 @@ __device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t
 }
 #undef TFRG_PREF_LOAD
 #undef TFRG_PREF_STORE
-
-// Medium records (lane_max < size, span <= kWStage): staged in LDS; CRC from LDS by all lanes;
-// the Features level walked once with scalar loads to list the map entries, then one entry per
-// lane (key lookup, Feature, list validation + count); anything else -> exact walk from LDS.
-template <bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kWaveBlock) void k_stage_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab,
-                                                           const uint32_t* __restrict__ consts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;         // [4][256] slice-by-4
-  uint32_t* A = lds + 1024;    // [4][256] (x) x^8192
-  uint32_t* cst = lds + 2048;  // [128] combine / unshift constants
-  uint32_t* kht = cst + 128;
-  uint32_t* krec = kht + kLdsMaxHt;
-  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
-  uint8_t* per_wave = reinterpret_cast<uint8_t*>(krec + kLdsMaxKeys * kKrWords);
-  const uint32_t ord_bytes = GORD ? 0u : ((sc.n_slots * 2u + 15u) & ~15u);
-  const uint32_t cnt_bytes = GORD ? 0u : ((sc.n_slots * 4u + 15u) & ~15u);
-  const uint32_t wave_bytes = kWStageStride + kMaxEnt * 4u + kLdsMaxKeys * 4u + ord_bytes + cnt_bytes;
-  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage = per_wave + wib * wave_bytes;
-  uint32_t* ent = reinterpret_cast<uint32_t*>(stage + kWStageStride);  // (len << 16) | off
-  uint32_t* kmark = reinterpret_cast<uint32_t*>(ent + kMaxEnt);
-  uint16_t* word = reinterpret_cast<uint16_t*>(kmark + kLdsMaxKeys);
-  uint32_t* wcnt = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(word) + ord_bytes);
-  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) lds[i] = crc_tab[i];
-  for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
-  if (fast_ok) {
-    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
-    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
-  }
-  __syncthreads();
-  const LdsTab<1> T{tab, 0};
-  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
-  const uint32_t nbig = o.info[kInfoBig];
-  const bool framed = !(B.flags & kFlagPayloadOnly);
-  const bool do_crc = framed && !(B.flags & kFlagNoCrc);
-  const uint32_t stride = gridDim.x * kWavesPerBlock;
-  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
-
-  // pipeline (RecPipe): bytes of i+stride, start/end of i+2*stride, index of i+3*stride in flight
-  RecPipe q;
-  q.r1 = i < nbig ? o.big_list[i] : 0u;
-  q.s1 = B.start[q.r1];
-  q.e1 = i < nbig ? B.end[q.r1] : 0ull;
-  Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
-  q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
-  q.s2v = B.start[vgpr_launder(q.r2)];
-  q.e2v = B.end[vgpr_launder(q.r2)];
-  q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
-  for (; i < nbig; i += stride) {
-    PHASE_MARK(t0);
-    const uint32_t r = q.r1;
-    const uint64_t en_raw = q.e1;
-    RecView v = rec_view_se(B, q.s1, q.e1);
-    const uint64_t lo16 = v.st & ~15ull;
-    pref_store(pf, stage, lo16, v.e, lane);
-    wave_lds_sync();
-    q.r1 = q.r2;
-    q.s1 = rfl64(q.s2v);
-    q.e1 = i + stride < nbig ? rfl64(q.e2v) : 0ull;
-    q.r2 = rfl32(q.r3v);
-    q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
-    pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
-    q.s2v = B.start[vgpr_launder(q.r2)];
-    q.e2v = B.end[vgpr_launder(q.r2)];
-
-    PHASE_MARK(t1);
-    int64_t aux = 0;
-    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, word), GORD ? B.n : 1u, 0, B.n, r, v.p0, false,
-                           lane == 0};
-    if constexpr (!GORD) sink.cnt = (lds_u32*)wcnt;
-    if (framed) {
-      const uint64_t D = v.e - v.st;
-      const uint32_t o0 = (uint32_t)(v.st - lo16);
-      if (D >= 8) {
-        const uint64_t lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
-        if (lenf == en_raw - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
-        if (do_crc && D >= 12) {
-          const uint32_t c = crc_lds<1>(stage, o0, o0 + 8, T);
-          if (crc_mask(c) == lds_u32u(stage, o0 + 8)) v.verdict |= TFRG_V_LEN_CRC;
-        }
-        if (do_crc && D >= 16) {
-          const uint32_t a = o0 + 12, b = (uint32_t)(v.e - lo16) - 4;
-          const uint32_t c = b - a < 64 ? crc_lds<1>(stage, a, b, T) : crc_wave_lds(stage, a, b, T, A, cst, lane);
-          if (crc_mask(c) == lds_u32u(stage, b)) v.verdict |= TFRG_V_DATA_CRC;
-        }
-      }
-    }
-    PHASE_MARK(t2);
-    for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
-    wave_lds_sync();
-    int status = kBail;
-    PHASE_ADD(0, t0, t1);
-    PHASE_ADD(1, t1, t2);
-    if (fast_ok) {
-      const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-      // phase A (scalar): the single Features field and its map entries
-      uint32_t n_ent = 0, fo = 0, fl = 0;
-      bool ok = hdr_0a(fs, 0, fo, fl) && fo + fl == fs.L;
-      for (uint32_t q = fo; ok && q < fs.L;) {
-        uint32_t eo, el;
-        if (n_ent >= kMaxEnt || !hdr_0a(fs, q, eo, el)) {
-          ok = false;
-          break;
-        }
-        if (lane == 0) ent[n_ent] = (el << 16) | eo;
-        ++n_ent;
-        q = eo + el;
-      }
-      PHASE_MARK(t3);
-      PHASE_ADD(3, t2, t3);
-      for (uint32_t k = lane; k < sc.n_keys; k += 64) kmark[k] = 0;
-      wave_lds_sync();
-      // phase B (64-wide): one entry per lane
-      bool lane_ok = true;
-      if (ok) {
-        for (uint32_t j = lane; j < n_ent; j += 64) {
-          const uint32_t en = ent[j];
-          int kid = -1, slot = -1;
-          uint32_t lo = 0, ll = 0, cnt = 0;
-          if (!entry_fast(fs, K, en & 0xffffu, en >> 16, kid, slot, lo, ll, cnt) ||
-              atomicAdd(&kmark[kid], 1u) != 0u) {  // duplicate key: exact path
-            lane_ok = false;
-            continue;
-          }
-          sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(j + 1);  // rank = entry position
-          const size_t at = (size_t)slot * B.n + r;
-          if constexpr (!GORD) sink.cnt[(size_t)slot * sink.ostride] = cnt;
-          else o.count[at] = cnt;
-          o.loc[at] = make_uint2(lo, ll);
-        }
-      }
-      wave_lds_sync();
-      if (ok && __ballot(!lane_ok) == 0) status = TFRG_OK;
-      PHASE_MARK(t4);
-      PHASE_ADD(4, t3, t4);
-    }
-    if (status == kBail) {  // exact, wave-uniform walk from the stage
-      for (uint32_t k = lane; k < sc.n_slots; k += 64) sink.ord[(size_t)k * sink.ostride] = 0;
-      wave_lds_sync();
-      sink.rank = 0;
-      LdsSrc s;
-      s.init(stage, lo16, v.p0, v.L);
-      status = walk_example<COMPAT>(s, sink, aux);
-      if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-      PHASE_ADD(8, 0, 1);
-    }
-    PHASE_MARK(t5);
-    wave_lds_sync();
-    wave_finalize(o, sink, sc.n_slots, B.n, r, status == TFRG_OK, lane);
-    if (lane == 0) record_result(o, r, status, aux, v.verdict);
-    wave_lds_sync();
-    PHASE_MARK(t6);
-    PHASE_ADD(6, t5, t6);
-    PHASE_ADD(7, t0, t6);
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Row-split scan, second level: per slot, exclusive scan of the 256-record tile sums in place (one
@@ -2278,9 +2010,6 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                               ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
   const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds;
   const size_t slow_lds = 2048ull * 4 + dict_lane;
-  const size_t wave_shared = (2048ull + 128 + kLdsMaxHt + (size_t)kLdsMaxKeys * kKrWords) * 4;
-  const size_t wave_per = (size_t)kWStageStride + kMaxEnt * 4 + kLdsMaxKeys * 4;
-  const size_t dict_wave = r16(S * 2) + r16(S * 4);
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
 
   mark(kStageLaneCount);
