@@ -1137,6 +1137,18 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
   return x;
 }
 
+// Wave-uniform values loaded with VECTOR loads: a laundered (VGPR) index keeps the compiler from
+// turning the load into a scalar one, whose lgkmcnt would be drained by every LDS wait of the walk.
+__device__ __forceinline__ uint32_t vgpr_launder(uint32_t x) {
+  uint32_t y;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
+  return y;
+}
+__device__ __forceinline__ uint32_t rfl32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
+  return ((uint64_t)rfl32((uint32_t)(x >> 32)) << 32) | rfl32((uint32_t)x);
+}
+
 // Lane-per-record FAST path. Each wave copies the contiguous span of its 64 records into its LDS
 // stage, then every lane checks its record's framing + CRC and runs the single-pass canonical walker
 // (fast_walk). Records the fast walker does not accept (non-canonical, erroneous, unknown keys), records
@@ -1172,6 +1184,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
 
   for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
        base += (uint64_t)gridDim.x * kLaneBlock) {
+    PHASE_MARK(p0);
     const uint64_t ri = base + lane;
     const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
@@ -1201,15 +1214,21 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
+    PHASE_MARK(p1);
+    PHASE_ADD(16, p0, p1);
     CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
                            GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
     if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
     bool done = false;
     if (staged && span_rec) {
       frame_verdicts<R, true>(B, v, T, stage, lo16);
+      PHASE_MARK(p2);
+      PHASE_ADD(17, p1, p2);
       for (uint32_t k = 0; k < S; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
       done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+      PHASE_MARK(p3);
+      PHASE_ADD(18, p2, p3);
     }
     // records above lane_max: the canonical walk straight from HBM, one record per lane (64 latency
     // chains in flight per wave); their payload CRC is k_wave_count's streaming pass
@@ -1222,6 +1241,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
         done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
       }
     }
+    PHASE_MARK(p4);
     // everything else of this wave's records goes to the exact walker
     const bool slow = valid && !done;
     const uint64_t sm = __ballot(slow);
@@ -1252,6 +1272,9 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       }
     }
     wave_lds_sync();  // the stage is rewritten by the next iteration
+    PHASE_MARK(p5);
+    PHASE_ADD(19, p4, p5);
+    PHASE_ADD(20, p0, p5);
   }
 }
 
@@ -1462,18 +1485,6 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     PHASE_MARK(h1);
     if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
   }
-}
-
-// Wave-uniform values loaded with VECTOR loads: a laundered (VGPR) index keeps the compiler from
-// turning the load into a scalar one, whose lgkmcnt would be drained by every LDS wait of the walk.
-__device__ __forceinline__ uint32_t vgpr_launder(uint32_t x) {
-  uint32_t y;
-  asm volatile("v_mov_b32 %0, %1" : "=v"(y) : "s"(x));
-  return y;
-}
-__device__ __forceinline__ uint32_t rfl32(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ uint64_t rfl64(uint64_t x) {
-  return ((uint64_t)rfl32((uint32_t)(x >> 32)) << 32) | rfl32((uint32_t)x);
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in

@@ -65,11 +65,12 @@ def main():
         from tfr_reader import _native
 
         L = _native.lib()
-        arr = (ctypes.c_ulonglong * 16)()
-        L.tfrg_debug_phase(arr, 16, 1)
+        arr = (ctypes.c_ulonglong * 32)()
+        L.tfrg_debug_phase(arr, 32, 1)
         names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
-                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane", "h.crc", "h.walk"]
-        tot = arr[7] or 1
+                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane", "h.crc", "h.walk", "-",
+                 "l.span+stage", "l.crc", "l.walk", "l.final", "l.total"]
+        tot = (arr[20] or arr[7]) or 1
         for i, nm in enumerate(names):
             print(f"{nm:10s} {arr[i]:>16d} {arr[i] / tot:8.3f}")
     info = dec.info()
