@@ -1402,7 +1402,8 @@ __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
 }
 
 // Horner over this wave's rounds j = J-1 .. 0, DEPTH rounds of loads in flight
-template <int DEPTH>
+// (STEP waves share a record: this wave's rounds are w + STEP j, its multiplier A = x^(8192 STEP))
+template <int DEPTH, int STEP>
 __device__ __forceinline__ uint32_t crc_rounds(const uint8_t* buf, uint64_t a, uint64_t b, int64_t c0, int64_t c1,
                                                int64_t J, const LdsTab<1>& T, const uint32_t* A4, uint32_t w,
                                                uint32_t lane) {
@@ -1412,7 +1413,7 @@ __device__ __forceinline__ uint32_t crc_rounds(const uint8_t* buf, uint64_t a, u
     int64_t chv[DEPTH];
 #pragma unroll
     for (int d = 0; d < DEPTH; ++d) {  // every load of the group in flight before any use
-      const int64_t k = (int64_t)w + 4 * (j - d);
+      const int64_t k = (int64_t)w + STEP * (j - d);
       const int64_t ch = c1 - 64 * k - (int64_t)lane;
       chv[d] = ch;
       const bool in = j - d >= 0 && ch >= c0;
@@ -1434,37 +1435,61 @@ __device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a
   const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
   const int64_t rounds = (c1 - c0 + 64) >> 6;
   const int64_t J = rounds > (int64_t)w ? (rounds - (int64_t)w + 3) / 4 : 0;  // rounds w + 4j, j < J
-  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth>(buf, a, b, c0, c1, J, T, A4, w, lane)
-                                     : crc_rounds<2>(buf, a, b, c0, c1, J, T, A4, w, lane);
+  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth, 4>(buf, a, b, c0, c1, J, T, A4, w, lane)
+                                     : crc_rounds<2, 4>(buf, a, b, c0, c1, J, T, A4, w, lane);
   uint32_t t = gf_mul(S, cst[lane]);  // chunk position inside its round: x^(128 l)
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
   return t;
 }
 
+// CRC-32C of a payload [a, b) (b - a >= 64) by one wave: consecutive 1 KiB rounds, x^8192 per step
+__device__ __forceinline__ uint32_t crc_one_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
+                                                 const uint32_t* A1, const uint32_t* cst, uint32_t lane) {
+  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
+  const int64_t J = (c1 - c0 + 64) >> 6;
+  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth, 1>(buf, a, b, c0, c1, J, T, A1, 0, lane)
+                                     : crc_rounds<2, 1>(buf, a, b, c0, c1, J, T, A1, 0, lane);
+  uint32_t t = gf_mul(S, cst[lane]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
+  const uint32_t z = (uint32_t)(16ull * (uint64_t)(c1 + 1) - b);
+  return ~gf_mul(t, cst[64 + z]);
+}
+
 // Payload CRC-32C of every record above lane_max (their framing bits and walk are the lane / slow
-// kernels'): one workgroup per record, the DATA_CRC verdict bit OR-ed into the verdict column.
+// kernels'), the DATA_CRC verdict bit OR-ed into the verdict column. Records whose span fits the
+// wave stage (the front of big_list) take one WAVE each; larger ones one WORKGROUP each.
 __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, const uint32_t* __restrict__ crc_tab,
                                                        const uint32_t* __restrict__ consts) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;           // [4][256] slice-by-4
-  uint32_t* A4 = lds + 1024;     // [4][256] (x) x^32768
-  uint32_t* cst = lds + 2048;    // [128] lane shifts x^(128 l), un-shifts x^(-8z), wave shifts x^(8192 w)
+  uint32_t* A1 = lds + 1024;     // [4][256] (x) x^8192
+  uint32_t* A4 = lds + 2048;     // [4][256] (x) x^32768
+  uint32_t* cst = lds + 3072;    // [128] lane shifts x^(128 l), un-shifts x^(-8z), wave shifts x^(8192 w)
   uint32_t* s_part = cst + 128;  // [4] wave sums
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nbig = o.info[kInfoBig], nhuge = o.info[kInfoHuge];
   if (B.flags & (kFlagPayloadOnly | kFlagNoCrc)) return;
-  if (blockIdx.x >= nbig + nhuge) return;  // workgroup-uniform
-  for (uint32_t i = threadIdx.x; i < 1024u; i += kWaveBlock) {
-    tab[i] = crc_tab[i];
-    A4[i] = crc_tab[4096 + i];
-  }
+  if (blockIdx.x * kWavesPerBlock >= nbig && blockIdx.x >= nhuge) return;  // workgroup-uniform
+  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) tab[i] = crc_tab[i];  // slice-by-4 + x^8192
+  for (uint32_t i = threadIdx.x; i < 1024u; i += kWaveBlock) A4[i] = crc_tab[4096 + i];
   for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  for (uint32_t i = blockIdx.x; i < nbig + nhuge; i += gridDim.x) {  // workgroup-uniform
+  // records within the wave stage size: one wave each
+  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
+    const uint32_t r = o.big_list[i];
+    const RecView v = rec_view(B, r);
+    if (v.e - v.st < 16) continue;
+    const uint64_t a = v.p0, b = v.e - 4;
+    const uint32_t c = b - a >= 64 ? crc_one_wave(B.bytes, a, b, T, A1, cst, lane) : crc_serial<1>(B.bytes, a, b, T);
+    if (lane == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
+  }
+  // larger records: one workgroup each
+  for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {  // workgroup-uniform
     PHASE_MARK(h0);
-    const uint32_t r = i < nbig ? o.big_list[i] : o.big_list[B.n - 1u - (i - nbig)];
+    const uint32_t r = o.big_list[B.n - 1u - i];
     const RecView v = rec_view(B, r);
     if (v.e - v.st < 16) continue;  // no payload CRC (lane_max below the framing size)
     const uint64_t a = v.p0, b = v.e - 4;
@@ -2053,7 +2078,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   mark(kStageWaveCount);
   {
     const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
-    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (2048 + 128 + 4) * 4, st, b, o, d_tab, d_consts);
+    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (3072 + 128 + 4) * 4, st, b, o, d_tab, d_consts);
   }
   mark(kStageSpine);
   if (S > 0) hipLaunchKernelGGL(k_spine, dim3(S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
