@@ -182,6 +182,24 @@ def test_c3_shape_vs_oracle(dec, orc):
     assert not _compare_to_oracle(r, orc, buf, st, en)
 
 
+def test_wide_schema_lane_records_vs_oracle(dec, orc):
+    """64-slot schema (MaskSink dict) with records below lane_max whose wave spans exceed the LDS
+    stage (canonical walk + serial CRC from HBM), a few corrupted."""
+    pl = synth.c3_payloads(700, seed=13, max_len=4)
+    buf, st, en = synth.framed(pl)
+    b = buf.copy()
+    for i in range(0, len(pl), 37):
+        b[int(st[i]) + 12 + (i % 50)] ^= 0x04
+    d = hip.HipDecoder(0)
+    try:
+        r = d.decode(b, st, en)
+        assert r.info.n_big == 0
+        bad = _compare_to_oracle(r, orc, b, st, en)
+    finally:
+        d.close()
+    assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("lane_max,wave_stage", [(0, 1 << 20), (0, 0), (1 << 20, 1 << 20)])
 def test_lane_and_wave_kernels_agree(dec, lane_max, wave_stage):
     pl = synth.c3_payloads(64, seed=11) + synth.c1_payloads(300) + synth.c2_payloads(8, seed=4, scale=0.1)

@@ -436,6 +436,26 @@ struct CountSinkT {
     return TFRG_OK;
   }
 
+  // canonical-walker interface (fast_walk)
+  __device__ __forceinline__ void fast_reset(uint32_t S) {
+    for (uint32_t k = 0; k < S; ++k) ord[(size_t)k * ostride] = 0;
+  }
+  __device__ __forceinline__ bool fast_taken(const uint32_t* kr) const {  // any kind of this key present
+    bool t = false;
+    for (int k = 0; k < 3; ++k) {
+      const int s2 = (int)kr[kKrSlot1 + k];
+      t |= s2 >= 0 && ord[(size_t)s2 * ostride] != 0;
+    }
+    return t;
+  }
+  __device__ __forceinline__ void fast_put(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
+    ord[(size_t)slot * ostride] = (uint16_t)rk;
+    const size_t at = (size_t)slot * n + r;
+    if constexpr (L) cnt[(size_t)slot * ostride] = cw;
+    else o->count[at] = cw;
+    o->loc[at] = lv;
+  }
+
   // final count of a present slot (LDS, or read back from this thread's own column write)
   __device__ __forceinline__ uint32_t count_of(uint32_t k) const {
     if constexpr (L) return cnt[(size_t)k * ostride];
@@ -463,6 +483,49 @@ __device__ __forceinline__ typename CountSinkT<L>::ord_t* dict_ord(uint16_t* glo
   if constexpr (L) return (lds_u16*)shared;
   else return global;
 }
+
+// Canonical-walker dict for schemas of <= 64 slots whose per-lane LDS dict does not fit: the order /
+// count / loc columns are written as the walk goes, the present slots kept in a 64-bit mask, and the
+// counts added to the wave's LDS tile sums (rolled back from the columns if the walk bails).
+struct MaskSink {
+  const DevOut* o;
+  uint32_t n, r;
+  lds_u32* tsl;  // [64] this wave's tile sums
+  uint64_t pm = 0;
+  uint32_t rank = 0;
+  __device__ __forceinline__ void fast_reset(uint32_t) { pm = 0; }
+  __device__ __forceinline__ bool fast_taken(const uint32_t* kr) const {
+    bool t = false;
+    for (int k = 0; k < 3; ++k) {
+      const int s2 = (int)kr[kKrSlot1 + k];
+      t |= s2 >= 0 && ((pm >> s2) & 1ull);
+    }
+    return t;
+  }
+  __device__ __forceinline__ void fast_put(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
+    const size_t at = (size_t)slot * n + r;
+    o->order[at] = (uint16_t)rk;
+    o->count[at] = cw;
+    o->loc[at] = lv;
+    pm |= 1ull << slot;
+    __atomic_fetch_add(&tsl[slot], cw & ~kCountInline, __ATOMIC_RELAXED);
+  }
+  __device__ __forceinline__ void rollback() {  // this thread's own column writes, read back
+    for (uint64_t m = pm; m; m &= m - 1) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(m);
+      __atomic_fetch_sub(&tsl[k], o->count[(size_t)k * n + r] & ~kCountInline, __ATOMIC_RELAXED);
+    }
+    pm = 0;
+  }
+  __device__ __forceinline__ void zero_absent(uint32_t S) {
+    for (uint32_t k = 0; k < S; ++k) {
+      if ((pm >> k) & 1ull) continue;
+      const size_t at = (size_t)k * n + r;
+      o->order[at] = 0;
+      o->count[at] = 0;
+    }
+  }
+};
 
 // ------------------------------------------------------------------------------------------------
 // CRC-32C helpers
@@ -1054,14 +1117,11 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
       ok &= !(seen & bit);
       seen |= bit;
     } else {
-      for (int k = 0; k < 3; ++k) {
-        const int s2 = (int)kr[kKrSlot1 + k];
-        ok &= !(s2 >= 0 && sink.ord[(size_t)s2 * sink.ostride]);
-      }
+      ok &= !sink.fast_taken(kr);
     }
     ok &= (slot >= 0) & (rank < 65534u);
     if (!ok) break;
-    sink.ord[(size_t)slot * sink.ostride] = (uint16_t)(++rank);
+    ++rank;
     // a single value goes inline into the loc word (int64 bits, float bits, bytes view)
     uint2 lv = make_uint2(lo, ll);
     uint32_t cw = cnt;
@@ -1079,10 +1139,7 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
         cw = 1u | kCountInline;
       }
     }
-    const size_t at = (size_t)slot * sink.n + sink.r;
-    if constexpr (Sink::kLds) sink.cnt[(size_t)slot * sink.ostride] = cw;
-    else sink.o->count[at] = cw;
-    sink.o->loc[at] = lv;
+    sink.fast_put((uint32_t)slot, rank, cw, lv);
   }
   sink.rank = rank;
   return ok ? TFRG_OK : kBail;
@@ -1156,13 +1213,15 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // above lane_max for the wavefront kernels. The per-slot value counts of the accepted records are
 // summed per 256-record tile (first level of the row-split scan).
 // GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
-template <int R, bool COMPAT, bool GORD>
+// MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
+template <int R, bool COMPAT, int MODE>
 __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;                                       // 256 * kLaneSlice * R dwords (slicing tables)
   uint32_t* cnt = lds + 256 * kLaneSlice * R;                // [n_slots][kLaneBlock]
+  constexpr bool GORD = MODE != 0;  // no per-lane LDS dict
   const uint32_t S = sc.n_slots;
   const uint32_t cnt_words = GORD ? 0u : S * kLaneBlock;
   uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneBlock]
@@ -1172,7 +1231,11 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
   uint8_t* stage = stage_all + wib * kStageStride;
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
+  lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
   for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  if constexpr (MODE == 1) {
+    tsl[lane] = 0;
+  }
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
@@ -1216,29 +1279,42 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
     }
     PHASE_MARK(p1);
     PHASE_ADD(16, p0, p1);
-    CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
-                           GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
-    if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
+    using SinkT = std::conditional_t<MODE == 1, MaskSink, CountSinkT<MODE == 0>>;
+    SinkT sink = [&]() {
+      if constexpr (MODE == 1) {
+        return MaskSink{&o, B.n, r, tsl};
+      } else {
+        CountSinkT<MODE == 0> c{&sc, &o, dict_ord<MODE == 0>(o.order + r, ord + threadIdx.x),
+                                GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
+        if constexpr (MODE == 0) c.cnt = (lds_u32*)(cnt + threadIdx.x);
+        return c;
+      }
+    }();
     bool done = false;
+    bool tried = false;
     if (staged && span_rec) {
       frame_verdicts<R, true>(B, v, T, stage, lo16);
       PHASE_MARK(p2);
       PHASE_ADD(17, p1, p2);
-      for (uint32_t k = 0; k < S; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+      sink.fast_reset(S);
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
       done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+      tried = true;
       PHASE_MARK(p3);
       PHASE_ADD(18, p2, p3);
     }
-    // records above lane_max: the canonical walk straight from HBM, one record per lane (64 latency
-    // chains in flight per wave); their payload CRC is k_wave_count's streaming pass
-    const bool bigw = fast_ok && valid && !mine;
+    // records above lane_max, and lane records of a wave whose span does not fit the stage: the
+    // canonical walk straight from HBM, one record per lane (64 latency chains in flight per wave).
+    // The payload CRC of records above lane_max is k_big_crc's streaming pass; the others' is
+    // computed here, serially per lane from HBM.
+    const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));
     if (__ballot(bigw)) {
       if (bigw) {
-        frame_verdicts<R, false>(B, v, T, nullptr, 0, false);
-        for (uint32_t k = 0; k < S; ++k) sink.ord[(size_t)k * sink.ostride] = 0;
+        frame_verdicts<R, false>(B, v, T, nullptr, 0, mine);
+        sink.fast_reset(S);
         const FastSrcG fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
         done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+        tried = true;
       }
     }
     PHASE_MARK(p4);
@@ -1257,6 +1333,19 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
     }
     // order / count columns of the accepted records + the tile sums (one atomic per slot and wave)
     const uint32_t tile = (uint32_t)(base >> kTileShift);
+    if constexpr (MODE == 1) {
+      if (tried && !done) sink.rollback();
+      if (done) sink.zero_absent(S);
+      wave_lds_sync();
+      if (lane < S) {
+        const uint32_t t = tsl[lane];
+        if (t) {
+          atomicAdd(&o.tsum[(size_t)lane * o.tile_stride + tile], t);
+          tsl[lane] = 0;
+        }
+      }
+    }
+    if constexpr (MODE != 1) {
     for (uint32_t k = 0; k < S; ++k) {
       const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
       const uint32_t c = ov ? sink.count_of(k) : 0u;
@@ -1270,6 +1359,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
         const uint32_t t = wave_sum_u32(x);
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
       }
+    }
     }
     wave_lds_sync();  // the stage is rewritten by the next iteration
     PHASE_MARK(p5);
@@ -2058,13 +2148,18 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     return g < cfg.lane_grid ? g : cfg.lane_grid;
   };
   if (lane_lds <= kLaneLdsBudget) {
-    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, false>);
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, false>), dim3(resident_grid(fn, lane_lds)), dim3(kLaneBlock),
+    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds)), dim3(kLaneBlock),
                        lane_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+  } else if (S <= 64) {
+    const size_t lds = tab_lds + stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4;
+    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
+                       st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else {
     const size_t lds = tab_lds + stage_lds + keys_lds;
-    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, true>);
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, true>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
+    const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageSlowCount);

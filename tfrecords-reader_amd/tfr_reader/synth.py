@@ -44,12 +44,12 @@ def c2_payloads(n: int = 8189, seed: int = 2, scale: float = 1.0) -> list[bytes]
     return out
 
 
-def c3_payloads(n: int = 8192, seed: int = 3) -> list[bytes]:
+def c3_payloads(n: int = 8192, seed: int = 3, max_len: int = 64) -> list[bytes]:
     rng = np.random.default_rng(seed)
     out = []
     for _ in range(n):
         feats = []
-        lens = rng.integers(0, 65, 64)
+        lens = rng.integers(0, max_len + 1, 64)
         for j in range(32):
             m = int(lens[j])
             bits = rng.integers(1, 32, m)
