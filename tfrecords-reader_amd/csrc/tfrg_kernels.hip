@@ -714,15 +714,15 @@ constexpr uint32_t kWStageStride = kWStage + 64;
 // copy absolute bytes [lo16, hi) (lo16 16-aligned) into dst
 __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
                                            uint32_t lane) {
-  // four 1 KiB wave-loads in flight per round, held in named registers (no scratch)
+  // four 1 KiB wave-loads in flight per round, unconditional (clamped addresses) so that all four
+  // are issued before the first wait, held in named registers (no scratch)
   for (uint32_t off = lane * 16u; lo16 + off < hi; off += 4096u) {
     const uint64_t q = lo16 + off;
     const bool h1 = q + 1024 < hi, h2 = q + 2048 < hi, h3 = q + 3072 < hi;
     const uint4 a = *reinterpret_cast<const uint4*>(src + q);
-    uint4 b = a, c = a, d = a;
-    if (h1) b = *reinterpret_cast<const uint4*>(src + q + 1024);
-    if (h2) c = *reinterpret_cast<const uint4*>(src + q + 2048);
-    if (h3) d = *reinterpret_cast<const uint4*>(src + q + 3072);
+    const uint4 b = *reinterpret_cast<const uint4*>(src + (h1 ? q + 1024 : q));
+    const uint4 c = *reinterpret_cast<const uint4*>(src + (h2 ? q + 2048 : q));
+    const uint4 d = *reinterpret_cast<const uint4*>(src + (h3 ? q + 3072 : q));
     *reinterpret_cast<uint4*>(dst + off) = a;
     if (h1) *reinterpret_cast<uint4*>(dst + off + 1024) = b;
     if (h2) *reinterpret_cast<uint4*>(dst + off + 2048) = c;
@@ -1245,16 +1245,29 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
   const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
 
-  for (uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u; base < B.n;
-       base += (uint64_t)gridDim.x * kLaneBlock) {
+  // the next iteration's offsets are requested before this iteration's stores (one HBM round trip
+  // less on the critical path of the next iteration)
+  const uint64_t lstride = (uint64_t)gridDim.x * kLaneBlock;
+  uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u;
+  uint64_t nst = 0, nen = 0;
+  if (base + lane < B.n) {
+    nst = B.start[base + lane];
+    nen = B.end[base + lane];
+  }
+  for (; base < B.n; base += lstride) {
     PHASE_MARK(p0);
     const uint64_t ri = base + lane;
     const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
+    const uint64_t cst0 = nst, cen0 = nen;
+    if (ri + lstride < B.n) {
+      nst = B.start[ri + lstride];
+      nen = B.end[ri + lstride];
+    }
     RecView v{};
     bool mine = false;
     if (valid) {
-      v = rec_view(B, r);
+      v = rec_view_se(B, cst0, cen0);
       const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
       if (big) {  // large record: wavefront kernels (staged ones from the front, huge from the back)
         if (v.e - (v.st & ~15ull) <= wave_stage) {
