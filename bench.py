@@ -120,12 +120,20 @@ def main() -> None:
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # TFRG_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin); the driver's runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("TFRG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if dist:
         import torch.distributed as tdist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
 
@@ -178,8 +186,9 @@ def main() -> None:
         tdist.barrier()
     ev_s = e0.elapsed_time(e1) / 1e3
     elapsed = max(wall, ev_s)
+    cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     info = dec.info()
@@ -288,8 +297,13 @@ def main() -> None:
 
     ms_step = elapsed / args.steps * 1e3
     gib_s_rank = framed_bytes / (ms_step / 1e3) / 2**30
-    value = framed_bytes * world / (elapsed / args.steps) / 2**30
-    ex_s = n * world / (elapsed / args.steps)
+    tot_bytes, tot_n = framed_bytes, n
+    if dist:  # every rank decodes its own shard: the whole job is the sum over ranks
+        t = torch.tensor([framed_bytes, n], dtype=torch.float64, device=cdev)
+        tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
+        tot_bytes, tot_n = float(t[0].item()), float(t[1].item())
+    value = tot_bytes / (elapsed / args.steps) / 2**30
+    ex_s = tot_n / (elapsed / args.steps)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
