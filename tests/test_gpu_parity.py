@@ -136,6 +136,34 @@ def test_c1_shape_vs_oracle(dec, orc):
     assert np.array_equal(labels, np.arange(65536) % 1000)
 
 
+def test_row_splits_across_spine_chunks(dec):
+    """2.6 M records = 3 chunks of the row-split scan (look-back across chunks), with every 7th
+    record of the second file lacking its label: row splits and values of both slots exact."""
+    from tests.golden.gen_golden import byt, entry, example
+
+    base = synth.c1_payloads(65536)
+    alt = [
+        example(entry(b"id", byt(f"img-{i:08d}".encode()))) if i % 7 == 0 else p
+        for i, p in enumerate(synth.c1_payloads(65536))
+    ]
+    buf0, st0, en0 = synth.framed(base + alt)
+    buf, st, en = synth.replicate(buf0, st0, en0, 20)
+    n = st.shape[0]
+    r = dec.decode(buf, st, en)
+    assert int(r.info.n_errors) == 0 and n > 2 * (1 << 20)
+    has = np.ones(131072, bool)
+    has[65536::7] = False
+    has = np.tile(has, 20)
+    lab = r.slot_key.index("label")
+    want_rs = np.concatenate([[0], np.cumsum(has)])
+    assert np.array_equal(r.row_splits[lab], want_rs)
+    want = np.tile(np.concatenate([np.arange(65536) % 1000, (np.arange(65536) % 1000)[np.arange(65536) % 7 != 0]]), 20)
+    got = r.i64[int(r.slot_base[lab]) : int(r.slot_base[lab]) + want.size]
+    assert np.array_equal(got, want)
+    ids = r.slot_key.index("id")
+    assert np.array_equal(r.row_splits[ids], np.arange(n + 1))
+
+
 def test_lane_crc_verdicts_every_alignment(dec, orc):
     """Lane-path CRC-32C over every payload length 9..200 and start alignment, with flipped bits in
     the length CRC, the payload and the data CRC of some records: verdicts, status and values vs
@@ -215,6 +243,71 @@ def test_wide_schema_lane_records_vs_oracle(dec, orc):
     finally:
         d.close()
     assert not bad, bad[:10]
+
+
+def _long_int_payloads(n, seed):
+    """Records holding long packed int64 lists (bodies past the wave-cooperative threshold) of mixed
+    varint widths (1..10 bytes, negatives included), some split over two chunks, some ending on a
+    continuation byte (malformed), next to short lists and a float list."""
+    from tests.golden.gen_golden import enc, entry, example, f32, i64, ld
+
+    rng = np.random.default_rng(seed)
+    out, vals_all = [], []
+    for i in range(n):
+        ents, vals = [], []
+        for j in range(int(rng.integers(1, 6))):
+            m = int(rng.choice([0, 1, 3, 40, 90, 200, 700]))
+            bits = rng.integers(1, 64, m)
+            v = [int(x) for x in (rng.random(m) * (2.0**bits)).astype(np.uint64) % (1 << 63)]
+            v = [-x if rng.random() < 0.1 else x for x in v]
+            body = b"".join(enc(x) for x in v)
+            if i % 11 == 3 and j == 0 and m > 2:  # two chunks: the per-lane walkers' case
+                h = len(enc(v[0]))
+                feat = ld(3, ld(1, body[:h]) + ld(1, body[h:]))
+            elif i % 13 == 5 and j == 0 and m > 2:  # last varint runs past its chunk
+                feat = ld(3, ld(1, body + b"\x81"))
+            else:
+                feat = i64(*v)
+            ents.append(entry(f"i{j}".encode(), feat))
+            vals.append(v)
+        ents.append(entry(b"f", f32(*rng.standard_normal(int(rng.integers(0, 100))).astype(np.float32).tolist())))
+        out.append(example(*ents))
+        vals_all.append(vals)
+    return out, vals_all
+
+
+def test_long_int64_lists_vs_oracle(dec, orc):
+    """Wave-cooperative decode of long packed int64 lists (records above lane_max) and its per-lane
+    fallbacks, in the reference's int-width varint mode: bit-exact vs the oracle."""
+    pl, _ = _long_int_payloads(300, seed=17)
+    buf, st, en = synth.framed(pl)
+    dec.set_lane_max(0)
+    try:
+        r = dec.decode(buf, st, en)
+    finally:
+        dec.set_lane_max(hip.DEFAULT_LANE_MAX)
+    assert r.info.n_big == len(pl)
+    bad = _compare_to_oracle(r, orc, buf, st, en)
+    assert not bad, bad[:10]
+
+
+def test_long_int64_lists_spec_mode():
+    """Same records with spec (64-bit) varints: the long lists decode to the encoded values."""
+    pl, vals = _long_int_payloads(120, seed=19)
+    buf, st, en = synth.framed(pl)
+    d = hip.HipDecoder(0, spec_varint=True)
+    try:
+        d.set_lane_max(0)
+        r = d.decode(buf, st, en)
+    finally:
+        d.close()
+    for i in range(len(pl)):
+        if i % 13 == 5:
+            continue  # malformed
+        assert int(r.status[i]) == 0, i
+        got = {k: v for k, _, v in raw_entries(r, i)}
+        for j, v in enumerate(vals[i]):
+            assert got[f"i{j}".encode()] == v, (i, j)
 
 
 @pytest.mark.parametrize("lane_max,wave_stage", [(0, 1 << 20), (0, 0), (1 << 20, 1 << 20)])

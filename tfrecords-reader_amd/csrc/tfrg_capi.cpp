@@ -287,13 +287,15 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   const uint64_t nn = n ? n : 1;
   const uint32_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
   const uint32_t tile_stride = (n_tiles + 3u) & ~3u;
+  const uint32_t n_chunks = (n_tiles + (1u << kSpineChunkShift) - 1u) >> kSpineChunkShift;
+  const uint64_t tsum_words = (uint64_t)S * tile_stride + 2ull * S * n_chunks;  // tile sums + look-back words
   const uint64_t cap_i64 = nbytes + 16, cap_f32 = nbytes / 4 + 16, cap_b = nbytes / 2 + 16;
   // growing an arena buffer frees the old one: wait for work that may still read it
   bool grow = c->status.cap < nn * 4 || c->aux.cap < nn * 8 || c->verdict.cap < nn ||
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
               c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
-              c->slow_list.cap < nn * 4 || c->tsum.cap < (uint64_t)S * tile_stride * 4 + 16;
+              c->slow_list.cap < nn * 4 || c->tsum.cap < tsum_words * 4 + 16;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
       c->count.ensure(S * nn * 4) || c->loc.ensure(S * nn * 8) || c->rs.ensure(S * (nn + 1) * 4) ||
@@ -301,14 +303,14 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
       c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->slow_list.ensure(nn * 4) ||
       c->miss.ensure(kMissCap * 16ull) || c->info.ensure(kInfoCount * 4) ||
-      c->tsum.ensure((uint64_t)S * tile_stride * 4 + 16)) {
+      c->tsum.ensure(tsum_words * 4 + 16)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
   // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
   HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
   HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
-  if (S && n) HIP_TRY(hipMemsetAsync(c->tsum.p, 0, (size_t)S * tile_stride * 4, st));
+  if (S && n) HIP_TRY(hipMemsetAsync(c->tsum.p, 0, tsum_words * 4, st));
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
   if (!S || !n) HIP_TRY(hipMemsetAsync(c->kind_totals.p, 0, 32, st));
 
@@ -343,6 +345,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.info = c->info.as<uint32_t>();
   o.tsum = c->tsum.as<uint32_t>();
   o.tile_stride = tile_stride;
+  o.spine_lb = reinterpret_cast<uint64_t*>(o.tsum + (size_t)S * tile_stride);  // 16-byte aligned
+  o.n_chunks = n_chunks;
   o.slow_list = c->slow_list.as<uint32_t>();
   LaunchCfg cfg;
   cfg.num_cus = c->num_cus;

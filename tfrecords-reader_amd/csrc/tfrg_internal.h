@@ -59,6 +59,7 @@ enum InfoIdx : uint32_t {
   kInfoSlow = 7,         // lane records left to the exact (slow) walker
   kInfoSpineDone = 8,    // spine workgroups finished (the last one computes the column bases)
   kInfoNeed = 9,         // lane records with an out-of-line list (k_list_gather; listed in slow_list)
+  kInfoSpineTicket = 10, // k_spine workgroup tickets (chunk order of the look-back)
   kInfoCount = 16
 };
 
@@ -87,6 +88,9 @@ struct DevOut {
   uint32_t* info;        // [kInfoCount]
   uint32_t* tsum;        // [n_slots][tile_stride] per-tile value counts, then their exclusive prefixes
   uint32_t tile_stride;  // >= n_tiles, multiple of 4
+  uint64_t* spine_lb;    // [n_slots][n_chunks] k_spine look-back words: flag << 32 | chunk total / inclusive
+                         // prefix (flag 1 / 2; zeroed per decode with tsum)
+  uint32_t n_chunks;     // ceil(n_tiles / 2^kSpineChunkShift)
   uint32_t* slow_list;   // [n] lane records for the exact walker; reused by k_down_gather for the
                          // records k_list_gather decodes (the slow list is consumed by then)
 };
@@ -94,6 +98,8 @@ struct DevOut {
 // Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)
 constexpr uint32_t kTileShift = 8;
 constexpr uint32_t kTileRecs = 1u << kTileShift;
+// k_spine chunks: 2^12 tiles (1 M records) per workgroup
+constexpr uint32_t kSpineChunkShift = 12;
 
 // flags (mirrors include/tfrg.h)
 constexpr uint32_t kFlagPayloadOnly = 1u;

@@ -11,7 +11,8 @@
 //                      schema misses) for the slow list, one lane per record.
 //   3. k_big_crc     : payload CRC of records above lane_max, one workgroup per record, the four
 //                      waves recombined with GF(2) shift operators (crc32c.h).
-//   4. k_spine       : per-slot exclusive scan of the tile sums + per-kind column bases.
+//   4. k_spine       : exclusive scan of the tile sums per (slot, chunk) with a decoupled look-back
+//                      across chunks; per-kind column bases (last workgroup).
 //   5. k_down_gather : row splits (tile prefix + in-tile scan) and inline single values.
 //   6. k_list_gather / k_stage_gather / k_wave_gather : out-of-line lists of lane records and of
 //                      records above lane_max.
@@ -1662,12 +1663,17 @@ __device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t
 #undef TFRG_PREF_STORE
 
 // ------------------------------------------------------------------------------------------------
-// Row-split scan, second level: per slot, exclusive scan of the 256-record tile sums in place (one
-// 1024-thread workgroup per slot, 16 tiles per thread per pass). The last workgroup to finish
+// Row-split scan, second level: the tile sums of every slot in chunks of 4096 tiles (1 M records),
+// one 256-thread workgroup per (slot, chunk), 16 tiles per thread, with a decoupled look-back
+// across the chunks of a slot: each workgroup publishes its chunk total (flag 1) at once, sums
+// its predecessors' totals back to the first inclusive prefix (flag 2), publishes its own
+// inclusive prefix and writes full exclusive prefixes over the tile sums in place. Chunks are
+// taken in ticket order, so every workgroup waited on has started. The last workgroup to finish
 // derives the per-kind column bases from the slot totals.
 // ------------------------------------------------------------------------------------------------
-constexpr int kSpineBlock = 1024;
+constexpr int kSpineBlock = 256;
 constexpr int kSpineItems = 16;
+static_assert(kSpineBlock * kSpineItems == (1 << kSpineChunkShift), "one chunk per spine workgroup");
 
 __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
 #pragma unroll
@@ -1678,68 +1684,108 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane
   return v;
 }
 
+// exclusive prefix of chunk `chunk` from its predecessors' look-back words (lb[0..chunk))
+__device__ __forceinline__ uint32_t spine_look_back(const uint64_t* lb, uint32_t chunk) {
+  uint32_t excl = 0;
+  for (int64_t j = (int64_t)chunk - 1; j >= 0;) {
+    const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t flag = (uint32_t)(w >> 32);
+    if (!flag) {  // predecessor still scanning (it has started: ticket order)
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += (uint32_t)w;
+    if (flag == 2u) break;
+    --j;
+  }
+  return excl;
+}
+
+// grid n_chunks * n_slots (1-D)
 __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* __restrict__ slot_kind, uint32_t n_slots,
                                                        uint32_t n_tiles) {
   __shared__ uint32_t s_w[kSpineBlock / 64];
-  __shared__ uint32_t s_last;
+  __shared__ uint32_t s_ticket, s_excl, s_last;
+  __shared__ uint32_t s_w2[kSpineBlock];  // last workgroup: slot totals of one pass
+  __shared__ uint8_t s_kind[kSpineBlock];
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
-  uint32_t* t = o.tsum + (size_t)blockIdx.x * o.tile_stride;
-  uint32_t carry = 0;
-  for (uint32_t b = 0; b < n_tiles; b += kSpineBlock * kSpineItems) {
-    const uint32_t i0 = b + threadIdx.x * kSpineItems;
-    uint32_t v[kSpineItems];
+  if (threadIdx.x == 0) s_ticket = atomicAdd(&o.info[kInfoSpineTicket], 1u);
+  __syncthreads();
+  const uint32_t slot = s_ticket / o.n_chunks, chunk = s_ticket % o.n_chunks;
+  uint32_t* t = o.tsum + (size_t)slot * o.tile_stride;
+  uint64_t* lb = o.spine_lb + (size_t)slot * o.n_chunks;
+  const uint32_t i0 = (chunk << kSpineChunkShift) + threadIdx.x * kSpineItems;
+  uint32_t v[kSpineItems];
 #pragma unroll
-    for (int j = 0; j < kSpineItems; j += 4) {  // tile_stride is a multiple of 4: whole uint4s are in bounds
-      uint4 q = make_uint4(0, 0, 0, 0);
-      if (i0 + j < n_tiles) q = *reinterpret_cast<const uint4*>(t + i0 + j);
-      v[j] = q.x;
-      v[j + 1] = i0 + j + 1 < n_tiles ? q.y : 0u;
-      v[j + 2] = i0 + j + 2 < n_tiles ? q.z : 0u;
-      v[j + 3] = i0 + j + 3 < n_tiles ? q.w : 0u;
-    }
-    uint32_t sum = 0;
+  for (int j = 0; j < kSpineItems; j += 4) {  // tile_stride is a multiple of 4: whole uint4s are in bounds
+    uint4 q = make_uint4(0, 0, 0, 0);
+    if (i0 + j < n_tiles) q = *reinterpret_cast<const uint4*>(t + i0 + j);
+    v[j] = q.x;
+    v[j + 1] = i0 + j + 1 < n_tiles ? q.y : 0u;
+    v[j + 2] = i0 + j + 2 < n_tiles ? q.z : 0u;
+    v[j + 3] = i0 + j + 3 < n_tiles ? q.w : 0u;
+  }
+  uint32_t sum = 0;
 #pragma unroll
-    for (int j = 0; j < kSpineItems; ++j) sum += v[j];
-    const uint32_t incl = wave_incl_scan_u32(sum, lane);
-    if (lane == 63) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t pre = carry, tot = 0;
+  for (int j = 0; j < kSpineItems; ++j) sum += v[j];
+  const uint32_t incl = wave_incl_scan_u32(sum, lane);
+  if (lane == 63) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kSpineBlock / 64; ++w) {
-      const uint32_t x = s_w[w];
-      pre += (uint32_t)w < wid ? x : 0u;
-      tot += x;
-    }
-    __syncthreads();
-    uint32_t run = pre + incl - sum;
-#pragma unroll
-    for (int j = 0; j < kSpineItems; j += 4) {
-      uint32_t w[4];
-#pragma unroll
-      for (int m = 0; m < 4; ++m) {
-        w[m] = run;
-        run += v[j + m];
-      }
-      if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    carry += tot;
+  for (int w = 0; w < kSpineBlock / 64; ++w) {
+    const uint32_t x = s_w[w];
+    pre += (uint32_t)w < wid ? x : 0u;
+    tot += x;
   }
   if (threadIdx.x == 0) {
-    o.totals[blockIdx.x] = carry;
-    __threadfence();
-    s_last = atomicAdd(&o.info[kInfoSpineDone], 1u) == n_slots - 1u;
+    __hip_atomic_store(&lb[chunk], ((uint64_t)(chunk ? 1u : 2u) << 32) | tot, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t excl = spine_look_back(lb, chunk);
+    if (chunk) __hip_atomic_store(&lb[chunk], (2ull << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (chunk == o.n_chunks - 1u) o.totals[slot] = excl + tot;
+    s_excl = excl;
   }
   __syncthreads();
-  if (s_last && threadIdx.x == 0) {  // every slot total is visible: column bases per kind
-    __threadfence();
-    uint64_t acc[4] = {0, 0, 0, 0};
-    for (uint32_t s = 0; s < n_slots; ++s) {
-      const uint32_t k = slot_kind[s] & 3u;
-      o.slot_base[s] = acc[k];
-      acc[k] += __hip_atomic_load(&o.totals[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t run = s_excl + pre + incl - sum;
+#pragma unroll
+  for (int j = 0; j < kSpineItems; j += 4) {
+    uint32_t w[4];
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      w[m] = run;
+      run += v[j + m];
     }
-    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+    if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(w[0], w[1], w[2], w[3]);
   }
+  if (threadIdx.x == 0) {
+    __threadfence();
+    s_last = atomicAdd(&o.info[kInfoSpineDone], 1u) == gridDim.x - 1u;
+  }
+  __syncthreads();
+  if (!s_last) return;  // workgroup-uniform
+  __threadfence();      // every slot total is visible
+  // per pass of 256 slots, thread 0 derives the per-kind column bases from LDS copies
+  uint64_t acc[4] = {0, 0, 0, 0};  // thread 0
+  for (uint32_t b = 0; b < n_slots; b += kSpineBlock) {
+    const uint32_t k = b + threadIdx.x;
+    if (k < n_slots) {
+      s_w2[threadIdx.x] = __hip_atomic_load(&o.totals[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_kind[threadIdx.x] = slot_kind[k] & 3u;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t m = n_slots - b < (uint32_t)kSpineBlock ? n_slots - b : (uint32_t)kSpineBlock;
+      for (uint32_t j = 0; j < m; ++j) {
+        const uint32_t kd = s_kind[j];
+        o.slot_base[b + j] = acc[kd];
+        acc[kd] += s_w2[j];
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2010,30 +2056,84 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int k) {
 // Values of up to 64 slots of one staged record (one slot per lane). Canonical packed float lists
 // are copied by the whole wave (lane j moves value j: contiguous stores); int64 and bytes lists
 // and anything non-canonical are decoded by their own lane.
+// Per-lane form of hdr_0a: the list at [lo, lo+ll) is exactly one canonical chunk (tag 0x0a, length
+// varint of <= 3 bytes) whose body is [bo, bo+bl).
+__device__ __forceinline__ bool hdr_0a_v(const FastSrc& s, uint32_t lo, uint32_t ll, uint32_t& bo, uint32_t& bl) {
+  const uint32_t w = lo + 2 <= s.L ? s.w4(lo) : 0u;
+  const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
+  const uint32_t h = b1 < 0x80u ? 2u : b2 < 0x80u ? 3u : 4u;
+  const uint32_t len = (b1 & 0x7fu) | (h > 2u ? (b2 & 0x7fu) << 7 : 0u) | (h > 3u ? (b3 & 0x7fu) << 14 : 0u);
+  bo = lo + h;
+  bl = len;
+  return (w & 0xffu) == 0x0au && (h < 4u || b3 < 0x80u) && bo + bl == lo + ll;
+}
+
+// Packed int64 lists of at least this many bytes are decoded by the whole wave (one byte per lane,
+// ~100 VALU per 64 bytes); shorter ones by their own lane (~40 VALU per value, all lanes in
+// parallel), which is cheaper when the record has many short lists (2.4 vs 3.3 ms).
+constexpr uint32_t kCoopIntBytes = 256;
+
 template <bool COMPAT>
 __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevOut& o, bool present, uint32_t kind,
-                                                   uint2 lc, uint64_t dst, uint64_t lo16, uint32_t lane) {
+                                                   uint2 lc, uint32_t cnt, uint64_t dst, uint64_t lo16,
+                                                   uint32_t lane) {
   PHASE_MARK(g0);
-  bool fail = false;
-  uint64_t m = __ballot(present && kind == TFRG_KIND_FLOAT && lc.y != 0u);
+  // every lane reads its own slot's chunk header up front: the wave loops below only readlane them
+  uint32_t bo = 0, bl = 0;
+  const bool packed = present && kind != TFRG_KIND_BYTES && hdr_0a_v(fs, lc.x, lc.y, bo, bl) &&
+                      (kind != TFRG_KIND_FLOAT || !(bl & 3u));
+  bool fail = present && kind != TFRG_KIND_BYTES && !packed;
+  // canonical float lists: lane j moves value j (contiguous 4-byte stores)
+  uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
   while (m) {
     const int k = __builtin_ctzll(m);
     m &= m - 1;
-    const uint32_t lo = __builtin_amdgcn_readlane(lc.x, k), ll = __builtin_amdgcn_readlane(lc.y, k);
+    const uint32_t b0 = __builtin_amdgcn_readlane(bo, k), nf = __builtin_amdgcn_readlane(bl, k) >> 2;
     const uint64_t d = readlane_u64(dst, k);
-    uint32_t bo, bl;
-    if (!hdr_0a(fs, lo, bo, bl) || bo + bl != lo + ll || (bl & 3u)) {
-      fail |= lane == (uint32_t)k;
-      continue;
+    for (uint32_t j = lane; j < nf; j += 64) {
+      if (d + j < o.cap_f32) o.f32[d + j] = lds_u32u(fs.l, fs.p + b0 + 4u * j);
     }
-    const uint32_t cnt = bl >> 2;
-    for (uint32_t j = lane; j < cnt; j += 64) {
-      if (d + j < o.cap_f32) o.f32[d + j] = lds_u32u(fs.l, fs.p + bo + 4u * j);
+  }
+  // long canonical packed int64 lists: 64 bytes per wave step, one byte per lane; a lane holding a
+  // terminator decodes the varint ending there (its start is the previous terminator + 1, from the
+  // ballot) and stores it at its index among the terminators. The chunk must end on a terminator
+  // and hold exactly the counted values, else that slot takes the per-lane path below (which
+  // rewrites the whole range; stores here never leave [dst, dst + cnt)).
+  const bool coop = packed && kind == TFRG_KIND_INT64 && bl >= kCoopIntBytes;
+  fail |= packed && kind == TFRG_KIND_INT64 && !coop;
+  m = __ballot(coop);
+  while (m) {
+    const int k = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint32_t b0 = __builtin_amdgcn_readlane(bo, k), nb = __builtin_amdgcn_readlane(bl, k);
+    const uint32_t c = __builtin_amdgcn_readlane(cnt, k);
+    const uint64_t d = readlane_u64(dst, k);
+    const uint32_t e = b0 + nb;
+    uint32_t done = 0, vst = b0;
+    bool bad = false;
+    for (uint32_t w0 = 0; w0 < nb; w0 += 64) {
+      const uint32_t j = w0 + lane;
+      const bool in = j < nb;
+      const uint32_t b = in ? fs.l[fs.p + b0 + j] : 0x80u;
+      const bool t = !(b & 0x80u);
+      const uint64_t tm = __ballot(t);
+      const uint64_t below = tm & ((1ull << lane) - 1ull);
+      if (t) {
+        uint32_t pos = below ? b0 + w0 + 64u - (uint32_t)__builtin_clzll(below) : vst;
+        const uint32_t idx = done + (uint32_t)__popcll(below);
+        int64_t v;
+        const bool okv = fast_value<COMPAT>(fs, pos, e, v) && pos == b0 + j + 1u;
+        if (okv && idx < c && d + idx < o.cap_i64) o.i64[d + idx] = v;
+        bad |= !okv;
+      }
+      done += (uint32_t)__popcll(tm);
+      if (tm) vst = b0 + w0 + 64u - (uint32_t)__builtin_clzll(tm);
     }
+    if (__ballot(bad) || done != c || vst != e) fail |= lane == (uint32_t)k;
   }
   PHASE_MARK(g1);
   PHASE_ADD(11, g0, g1);
-  if (present && (kind != TFRG_KIND_FLOAT || fail)) {
+  if (present && (kind == TFRG_KIND_BYTES || fail)) {
     if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst)) {
       LdsSrc s;
       s.init(fs.l, lo16, fs.base, fs.L);
@@ -2074,12 +2174,12 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
     wave_lds_sync();
     // slot metadata of this record (issued ahead of the next record's byte loads)
     bool present = false;
-    uint32_t kind = 0;
+    uint32_t kind = 0, c = 0;
     uint2 lc = make_uint2(0, 0);
     uint64_t dst = 0;
     if (ok && lane < sc.n_slots) {
       const size_t at = (size_t)lane * B.n + r;
-      const uint32_t c = o.count[at];
+      c = o.count[at];
       present = c && !(c & kCountInline);  // inline single values are k_down_gather's
       lc = o.loc[at];
       dst = o.slot_base[lane] + o.rs[(size_t)lane * (B.n + 1) + r];
@@ -2099,22 +2199,22 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
     PHASE_MARK(t1);
     PHASE_ADD(9, t0, t1);
     const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-    stage_gather_group<COMPAT>(fs, o, present, kind, lc, dst, lo16, lane);
+    stage_gather_group<COMPAT>(fs, o, present, kind, lc, c, dst, lo16, lane);
     for (uint32_t kb = 64; kb < sc.n_slots; kb += 64) {  // wide schemas: further groups of 64 slots
       const uint32_t k = kb + lane;
       bool pk = false;
-      uint32_t kk = 0;
+      uint32_t kk = 0, ck = 0;
       uint2 lk = make_uint2(0, 0);
       uint64_t dk = 0;
       if (k < sc.n_slots) {
         const size_t at = (size_t)k * B.n + r;
-        const uint32_t c = o.count[at];
-        pk = c && !(c & kCountInline);
+        ck = o.count[at];
+        pk = ck && !(ck & kCountInline);
         lk = o.loc[at];
         dk = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
         kk = sc.slot_kind[k];
       }
-      stage_gather_group<COMPAT>(fs, o, pk, kk, lk, dk, lo16, lane);
+      stage_gather_group<COMPAT>(fs, o, pk, kk, lk, ck, dk, lo16, lane);
     }
     wave_lds_sync();
     PHASE_MARK(t2);
@@ -2189,7 +2289,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (3072 + 128 + 4) * 4, st, b, o, d_tab, d_consts);
   }
   mark(kStageSpine);
-  if (S > 0) hipLaunchKernelGGL(k_spine, dim3(S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
+  if (S > 0)
+    hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
   mark(kStageDownGather);
   if (S > 0) {
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus)
@@ -2205,8 +2306,13 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        cfg.lane_max);
   mark(kStageWaveGather);
   if (S > 0) {
-    hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock),
-                       (size_t)kWStageStride * kWavesPerBlock, st, b, sc, o);
+    const size_t lds = (size_t)kWStageStride * kWavesPerBlock;
+    const void* fn = reinterpret_cast<const void*>(&k_stage_gather<COMPAT>);
+    int per_cu = 0;  // one round of resident workgroups (3 per CU: a second round would run at 1/3)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
+    hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, sc, o);
     hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
   }
   mark(kNumStages);
