@@ -533,12 +533,39 @@ struct MaskSink {
 // ------------------------------------------------------------------------------------------------
 // LDS table view with R-fold bank replication: entry (j, v) copy c at dword ((j*256+v)*R + c).
 // Lane l reads copy l % R, so up to R lanes of a 32-lane group never collide on a bank.
+// ((x >> 8K) & 0xff) * 4 in one VALU: a shift with an SDWA byte select of its source
+template <int K>
+__device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
+  static_assert(K >= 0 && K < 4, "byte index");
+  uint32_t r;
+  const uint32_t two = 2u;
+  if constexpr (K == 0)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+        : "=v"(r) : "v"(two), "v"(x));
+  else if constexpr (K == 1)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+        : "=v"(r) : "v"(two), "v"(x));
+  else if constexpr (K == 2)
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2"
+        : "=v"(r) : "v"(two), "v"(x));
+  else
+    asm("v_lshlrev_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3"
+        : "=v"(r) : "v"(two), "v"(x));
+  return r;
+}
+
 template <int R>
 struct LdsTab {
   const uint32_t* t;
   uint32_t c;
   __device__ __forceinline__ uint32_t operator()(uint32_t j, uint32_t v) const { return t[((j << 8) + v) * R + c]; }
+  // entry of table j at byte offset bx4 = 4 * index
+  __device__ __forceinline__ uint32_t at4(uint32_t j, uint32_t bx4) const {
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(t) + (j << 10) + bx4);
+  }
   __device__ __forceinline__ uint32_t step4(uint32_t x) const {
+    if constexpr (R == 1)  // table byte offsets in one SDWA instruction each (the lane kernel is VALU-bound)
+      return at4(3, byte_x4<0>(x)) ^ at4(2, byte_x4<1>(x)) ^ at4(1, byte_x4<2>(x)) ^ at4(0, byte_x4<3>(x));
     return (*this)(3, x & 0xffu) ^ (*this)(2, (x >> 8) & 0xffu) ^ (*this)(1, (x >> 16) & 0xffu) ^ (*this)(0, x >> 24);
   }
   __device__ __forceinline__ uint32_t step1(uint32_t c_, uint32_t byte) const {
@@ -659,7 +686,10 @@ __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int s
 // with coalesced 16-byte loads (1 KiB per wave-instruction) and every lane then parses its record
 // from LDS instead of issuing scattered, latency-bound global loads.
 // ------------------------------------------------------------------------------------------------
-constexpr uint32_t kStageBytes = 4096;                // span capacity per wave
+#ifndef TFRG_STAGE_BYTES
+#define TFRG_STAGE_BYTES 4096
+#endif
+constexpr uint32_t kStageBytes = TFRG_STAGE_BYTES;    // span capacity per wave
 constexpr uint32_t kStageStride = kStageBytes + 64;   // + slack for aligned over-reads at the tail
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
@@ -1220,8 +1250,9 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;                                       // 256 * kLaneSlice * R dwords (slicing tables)
-  uint32_t* cnt = lds + 256 * kLaneSlice * R;                // [n_slots][kLaneBlock]
+  // slicing tables at a static LDS address: lookups fold the table base into the ds_read offset
+  __shared__ uint32_t tab[256 * kLaneSlice * R];
+  uint32_t* cnt = lds;                                       // [n_slots][kLaneBlock]
   constexpr bool GORD = MODE != 0;  // no per-lane LDS dict
   const uint32_t S = sc.n_slots;
   const uint32_t cnt_words = GORD ? 0u : S * kLaneBlock;
@@ -2262,15 +2293,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   };
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds)), dim3(kLaneBlock),
-                       lane_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
+                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else if (S <= 64) {
-    const size_t lds = tab_lds + stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4;
+    const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else {
-    const size_t lds = tab_lds + stage_lds + keys_lds;
+    const size_t lds = stage_lds + keys_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
