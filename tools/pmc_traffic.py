@@ -30,10 +30,14 @@ def run_pass(out: Path, counter: str, config: str) -> Path:
 
 
 def per_launch(path: Path, want: str) -> tuple[str, float]:
+    """Mean counter value over the full-batch dispatches of the kernel: the largest grid, and of
+    those the ones lasting at least half the longest (a resident-grid kernel has the same grid on
+    bench.py's small sample batch, which would otherwise be averaged in)."""
     rows = [r for r in csv.DictReader(open(path)) if want in r["Kernel_Name"]]
     grid = max(int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]) for r in rows)
-    vals = [float(r["Counter_Value"]) for r in rows
-            if int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]) == grid]
+    rows = [r for r in rows if int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]) == grid]
+    dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    vals = [float(r["Counter_Value"]) for r, d in zip(rows, dur) if d * 2 >= max(dur)]
     return rows[0]["Kernel_Name"], sum(vals) / len(vals)
 
 
