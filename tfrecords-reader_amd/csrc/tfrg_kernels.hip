@@ -1084,6 +1084,12 @@ __device__ __forceinline__ bool hdr2(const S& s, uint32_t pos, uint32_t end, uin
                                      uint32_t& len) {
   pos = pos < s.L ? pos : s.L;
   const uint32_t w = s.u32(pos);
+  if (__builtin_expect((w & 0x8087u) == 0x0002u, 1)) {  // 1-byte length (< 128): a third of the VALU
+    fn = (w >> 3) & 0xfu;
+    off = pos + 2u;
+    len = (w >> 8) & 0x7fu;
+    return off + len <= end;  // (pos <= L < 2^31: no wrap)
+  }
   const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
   const uint32_t c1 = b1 >> 7, c12 = c1 & (b2 >> 7);
   uint32_t l = b1 & 0x7fu;
