@@ -29,13 +29,24 @@ constexpr uint32_t kLdsMaxHt = 1024;      // hash-table entries staged into LDS
 
 // Key hash over (length, first 4 bytes, last 4 bytes), all little-endian and zero padded:
 // w0 = bytes [0, min(n,4)), w1 = n > 4 ? bytes [n-4, n) : 0. For n <= 8 the triple (n, w0, w1)
-// IS the key, so a table hit needs no byte compare.
+// IS the key, so a table hit needs no byte compare. Every input bit is folded into 24-bit
+// operands so that the device multiplies are full-rate v_mul_u32_u24 (v_mul_lo_u32 is quarter
+// rate, and the lane kernel is VALU-bound).
 __host__ __device__ inline uint32_t key_hash_words(uint32_t n, uint32_t w0, uint32_t w1) {
-  uint32_t h = n * 0x9E3779B1u;
-  h ^= w0 * 0x85EBCA77u;
-  h = (h << 13) | (h >> 19);
-  h ^= w1 * 0xC2B2AE3Du;
-  return h ^ (h >> 16);
+  const uint32_t a = (w0 ^ (w0 >> 11) ^ (n << 17)) & 0xffffffu;
+  const uint32_t b = (w1 ^ (w1 >> 13) ^ (n << 7)) & 0xffffffu;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // = the host's products mod 2^32 (both operands < 2^24); spelled out because the backend picks
+  // the quarter-rate v_mul_lo_u32 for these once the masks are reassociated
+  uint32_t p0, p1;
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p0) : "v"(a), "v"(0x9E3779u));
+  asm("v_mul_u32_u24 %0, %1, %2" : "=v"(p1) : "v"(b), "v"(0x85EBCBu));
+  uint32_t h = p0 ^ p1;
+#else
+  uint32_t h = a * 0x9E3779u;
+  h ^= b * 0x85EBCBu;
+#endif
+  return h ^ (h >> 15);
 }
 
 struct DevBatch {

@@ -870,6 +870,14 @@ struct FastSrcG {
   }
 };
 
+// 7-bit groups of the bytes of w selected by byte mask m, compacted (a varint of <= 4 bytes)
+__device__ __forceinline__ uint32_t vgroups(uint32_t w, uint32_t m) {
+  w &= m;
+  return (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
+}
+// byte mask of the first nb (1..4) bytes: shifts only (a multiply by 7 would be quarter rate)
+__device__ __forceinline__ uint32_t bytes_mask(uint32_t nb) { return nb >= 4u ? 0xffffffffu : (1u << (nb << 3)) - 1u; }
+
 // varint of <= 4 bytes (values < 2^28: identical in compat and spec mode); false = bail
 __device__ __forceinline__ bool fv32(const FastSrc& s, uint32_t& pos, uint32_t& v) {
   if (pos > s.L) return false;
@@ -877,8 +885,7 @@ __device__ __forceinline__ bool fv32(const FastSrc& s, uint32_t& pos, uint32_t& 
   const uint32_t term = ~w & 0x80808080u;
   if (!term) return false;
   const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
-  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-  v = x & ((1u << (7u * nb)) - 1u);
+  v = vgroups(w, term ^ (term - 1u));  // bytes up to the first terminator
   pos += nb;
   return true;
 }
@@ -990,7 +997,9 @@ __device__ __forceinline__ int fast_lookup(const S& s, const LdsKeys& K, uint32_
     const uint32_t e = K.ht[j];
     if (!e) return -1;
     const uint32_t* r = K.rec + (e - 1) * kKrWords;
-    if (r[kKrHash] == h && r[kKrLen] == kl && r[kKrW0] == w0 && r[kKrW1] == w1) {
+    const uint4 q = *reinterpret_cast<const uint4*>(r);  // (hash, len, w0, w1): one 16-byte read
+    static_assert(kKrHash == 0 && kKrLen == 1 && kKrW0 == 2 && kKrW1 == 3, "record head layout");
+    if ((q.x == h) & (q.y == kl) & (q.z == w0) & (q.w == w1)) {
       // (length, first 4, last 4) identify keys of <= 8 bytes; longer ones compare the middle too
       bool eq = true;
       if (kl > 8u) {
@@ -1015,8 +1024,7 @@ __device__ __forceinline__ bool fast_value(const FastSrc& s, uint32_t& pos, uint
   if (term) {
     const uint32_t nb = (__builtin_ctz(term) >> 3) + 1u;
     if (pos + nb > e) return false;
-    const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-    val = (int64_t)(x & ((1u << (7u * nb)) - 1u));
+    val = (int64_t)vgroups(w, term ^ (term - 1u));
     pos += nb;
     return true;
   }
@@ -1069,8 +1077,7 @@ __device__ __forceinline__ bool fast_single(const FastSrc& s, uint32_t kind, uin
   const uint32_t w = s.w4(co);
   const uint32_t term = ~w & 0x80808080u;
   if (!term || (__builtin_ctz(term) >> 3) + 1u != cl) return false;
-  const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-  val = make_uint2(x & ((1u << (7u * cl)) - 1u), 0u);
+  val = make_uint2(vgroups(w, bytes_mask(cl)), 0u);
   return true;
 }
 
@@ -1171,8 +1178,7 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
         cw = 1u | kCountInline;
       } else if (c0l <= 4u) {  // one varint of <= 4 bytes: value < 2^28, same in both varint modes
         const uint32_t w = s.u32(c0o);
-        const uint32_t x = (w & 0x7fu) | ((w >> 1) & 0x3f80u) | ((w >> 2) & 0x1fc000u) | ((w >> 3) & 0xfe00000u);
-        lv = make_uint2(x & ((1u << (7u * c0l)) - 1u), 0u);
+        lv = make_uint2(vgroups(w, bytes_mask(c0l)), 0u);
         cw = 1u | kCountInline;
       }
     }
