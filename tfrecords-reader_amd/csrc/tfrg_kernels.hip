@@ -1130,27 +1130,34 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
     if (!ok) break;
     const int kid = fast_lookup(s, K, ko, kl);
     // list chunks (field #1, packed); the first chunk's single value is kept for the inline path
-    uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0;
+    uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0, c0w = 0;
     const uint32_t le = lo + ll;
     for (uint32_t g = lo; ok && g < le;) {
       uint32_t cf, co, cl;
       ok = hdr2(s, g, le, cf, co, cl) & (cf == 1u);
       g = co + cl;
-      if (nch == 0) {
-        c0o = co;
-        c0l = cl;
-      }
-      ++nch;
       if (kind == TFRG_KIND_BYTES) {
         ++cnt;
       } else if (kind == TFRG_KIND_FLOAT) {
         ok &= (cl & 3u) == 0u;
         cnt += cl >> 2;
+      } else if (cl <= 4u) {  // one word: its terminators; the chunk must end on one
+        const uint32_t m = bytes_mask(cl);
+        const uint32_t w = s.u32(co) & m;
+        const uint32_t tm = ~w & 0x80808080u & m;
+        ok &= cl == 0u || ((tm >> ((cl << 3) - 1u)) & 1u);
+        cnt += __popc(tm);
+        if (nch == 0) c0w = w;
       } else {
         uint32_t k = 0;
         ok &= count_packed(s, co, co + cl, k);
         cnt += k;
       }
+      if (nch == 0) {
+        c0o = co;
+        c0l = cl;
+      }
+      ++nch;
     }
     ok &= kid >= 0;
     if (!ok) break;
@@ -1177,8 +1184,7 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
         lv = make_uint2(s.u32(c0o), 0u);
         cw = 1u | kCountInline;
       } else if (c0l <= 4u) {  // one varint of <= 4 bytes: value < 2^28, same in both varint modes
-        const uint32_t w = s.u32(c0o);
-        lv = make_uint2(vgroups(w, bytes_mask(c0l)), 0u);
+        lv = make_uint2(vgroups(c0w, 0xffffffffu), 0u);  // (the chunk's word, masked to c0l bytes)
         cw = 1u | kCountInline;
       }
     }
