@@ -1418,8 +1418,9 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
         o.count[at] = c;
       }
       const uint32_t x = c & ~kCountInline;
-      if (__ballot(x != 0u)) {
-        const uint32_t t = wave_sum_u32(x);
+      const uint64_t nz = __ballot(x != 0u);
+      if (nz) {  // counts of 0/1 (single values): the sum is a popcount of the ballot (scalar)
+        const uint32_t t = __ballot(x > 1u) ? wave_sum_u32(x) : (uint32_t)__popcll(nz);
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
       }
     }
