@@ -1984,7 +1984,9 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
 #pragma unroll
       for (uint32_t g = 0; g < kDG; ++g) {
         const uint32_t x = c[t][g] & ~kCountInline;
-        const uint32_t incl = wave_incl_scan_u32(x, lane);
+        // 0/1 counts (single values): the inclusive scan is a masked popcount of the ballot
+        const uint32_t incl = __ballot(x > 1u) ? wave_incl_scan_u32(x, lane)
+                                               : (uint32_t)__popcll(__ballot(x != 0u) & (~0ull >> (63u - lane)));
         ex[t][g] = incl - x;
         if (lane == 63) s_w[buf][t * kDG + g][wib] = incl;
       }
