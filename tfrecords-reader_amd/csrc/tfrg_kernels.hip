@@ -742,22 +742,26 @@ __device__ __forceinline__ void wave_lds_sync() {
 constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave (wavefront kernels)
 constexpr uint32_t kWStageStride = kWStage + 64;
 
-// copy absolute bytes [lo16, hi) (lo16 16-aligned) into dst
+// copy absolute bytes [lo16, hi) (lo16 16-aligned, wave-uniform, hi - lo16 <= kStageBytes) into dst
 __device__ __forceinline__ void stage_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi,
                                            uint32_t lane) {
-  // four 1 KiB wave-loads in flight per round, unconditional (clamped addresses) so that all four
+  // scalar base + 32-bit lane offsets: the address arithmetic stays off the (busy) VALU
+  const uint64_t l0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lo16 >> 32)) << 32) |
+                      __builtin_amdgcn_readfirstlane((uint32_t)lo16);
+  const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)(hi - lo16));
+  const uint8_t* base = src + l0;
+  // four 1 KiB wave-loads in flight per round, unconditional (clamped offsets) so that all four
   // are issued before the first wait, held in named registers (no scratch)
-  for (uint32_t off = lane * 16u; lo16 + off < hi; off += 4096u) {
-    const uint64_t q = lo16 + off;
-    const bool h1 = q + 1024 < hi, h2 = q + 2048 < hi, h3 = q + 3072 < hi;
-    const uint4 a = *reinterpret_cast<const uint4*>(src + q);
-    const uint4 b = *reinterpret_cast<const uint4*>(src + (h1 ? q + 1024 : q));
-    const uint4 c = *reinterpret_cast<const uint4*>(src + (h2 ? q + 2048 : q));
-    const uint4 d = *reinterpret_cast<const uint4*>(src + (h3 ? q + 3072 : q));
+  for (uint32_t off = lane * 16u; off < n; off += 4096u) {
+    const bool h1 = off + 1024u < n, h2 = off + 2048u < n, h3 = off + 3072u < n;
+    const uint4 a = *reinterpret_cast<const uint4*>(base + off);
+    const uint4 b = *reinterpret_cast<const uint4*>(base + (h1 ? off + 1024u : off));
+    const uint4 c = *reinterpret_cast<const uint4*>(base + (h2 ? off + 2048u : off));
+    const uint4 d = *reinterpret_cast<const uint4*>(base + (h3 ? off + 3072u : off));
     *reinterpret_cast<uint4*>(dst + off) = a;
-    if (h1) *reinterpret_cast<uint4*>(dst + off + 1024) = b;
-    if (h2) *reinterpret_cast<uint4*>(dst + off + 2048) = c;
-    if (h3) *reinterpret_cast<uint4*>(dst + off + 3072) = d;
+    if (h1) *reinterpret_cast<uint4*>(dst + off + 1024u) = b;
+    if (h2) *reinterpret_cast<uint4*>(dst + off + 2048u) = c;
+    if (h3) *reinterpret_cast<uint4*>(dst + off + 3072u) = d;
   }
 }
 
