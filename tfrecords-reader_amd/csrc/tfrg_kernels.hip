@@ -1210,9 +1210,12 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   const uint64_t D = v.e - v.st;
   if (D < 8) return;
   uint64_t lenf;
+  uint32_t lw0 = 0, lw1 = 0;
   if constexpr (STAGED) {
     const uint32_t o0 = (uint32_t)(v.st - lo16);
-    lenf = (uint64_t)lds_u32u(stage, o0) | ((uint64_t)lds_u32u(stage, o0 + 4) << 32);
+    lw0 = lds_u32u(stage, o0);
+    lw1 = lds_u32u(stage, o0 + 4);
+    lenf = (uint64_t)lw0 | ((uint64_t)lw1 << 32);
   } else {
     lenf = load_u64_unaligned(B.bytes, v.st);
   }
@@ -1220,7 +1223,8 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   if (do_crc && D >= 12) {
     uint32_t c, stored;
     if constexpr (STAGED) {
-      c = crc_lds8<R>(stage, (uint32_t)(v.st - lo16), (uint32_t)(v.st - lo16) + 8, T);
+      // the 8 length bytes are the two words just read: two slicing steps, any alignment
+      c = ~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1);
       stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
     } else {
       c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
