@@ -810,9 +810,16 @@ __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint3
       hm = 0xffffffffu;
     }
   } else {  // slice-by-4: the smaller table leaves LDS for more resident waves
-    for (; p + 8 <= bw; p += 4) {
+    for (; p + 12 <= bw; p += 8) {  // two words per iteration (one ds_read2, half the loop overhead)
+      const uint32_t x0 = w[p >> 2], x1 = w[(p >> 2) + 1];
+      c = T.step4(c ^ (x0 & hm));
+      hm = 0xffffffffu;
+      c = T.step4(c ^ x1);
+    }
+    if (p + 8 <= bw) {
       c = T.step4(c ^ (w[p >> 2] & hm));
       hm = 0xffffffffu;
+      p += 4;
     }
   }
   if (p + 4 <= bw) {
