@@ -292,7 +292,7 @@ def main() -> None:
     tf = REPO / "profiles" / f"traffic_{args.config}.json"
     if tf.is_file():
         t = json.loads(tf.read_text())
-        if dominant in t.get("kernel", "") and args.files is None:
+        if (dominant in t.get("kernel", "") or dominant == t.get("stage")) and args.files is None:
             traffic, traffic_src = int(t["traffic_bytes"]), f"profiles/{tf.name}"
 
     ms_step = elapsed / args.steps * 1e3
