@@ -1955,11 +1955,21 @@ __device__ __forceinline__ bool fast_list_gather(const FastSrc& s, const DevOut&
     } else {
       uint32_t p = co;
       const uint32_t e = co + cl;
-      while (p < e) {
-        int64_t v;
-        if (!fast_value<COMPAT>(s, p, e, v)) return false;
-        if (dst < o.cap_i64) o.i64[dst] = v;
-        ++dst;
+      if (dst + cl <= o.cap_i64) {  // at most cl values: no per-value capacity check, a running pointer
+        int64_t* out = o.i64 + dst;
+        while (p < e) {
+          int64_t v;
+          if (!fast_value<COMPAT>(s, p, e, v)) return false;
+          *out++ = v;
+        }
+        dst = (uint64_t)(out - o.i64);
+      } else {
+        while (p < e) {
+          int64_t v;
+          if (!fast_value<COMPAT>(s, p, e, v)) return false;
+          if (dst < o.cap_i64) o.i64[dst] = v;
+          ++dst;
+        }
       }
     }
   }
