@@ -1,5 +1,6 @@
+# GPU box: gpu tests + bench summary lines for CFGS (default c1): CFGS="c1 c2" bash tools/quick_check.sh
 set -u
-O=gpurun_out/tmp; mkdir -p $O
+O=gpurun_out/quick; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for c in ${CFGS:-c1}; do
