@@ -2172,8 +2172,9 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int k) {
 }
 
 // Values of up to 64 slots of one staged record (one slot per lane). Canonical packed float lists
-// are copied by the whole wave (lane j moves value j: contiguous stores); int64 and bytes lists
-// and anything non-canonical are decoded by their own lane.
+// are copied by the whole wave (lane j moves value j: contiguous stores), canonical packed int64
+// lists are decoded by the whole wave (int64_balanced); bytes lists and anything non-canonical are
+// decoded by their own lane.
 // Per-lane form of hdr_0a: the list at [lo, lo+ll) is exactly one canonical chunk (tag 0x0a, length
 // varint of <= 3 bytes) whose body is [bo, bo+bl).
 __device__ __forceinline__ bool hdr_0a_v(const FastSrc& s, uint32_t lo, uint32_t ll, uint32_t& bo, uint32_t& bl) {
@@ -2186,10 +2187,126 @@ __device__ __forceinline__ bool hdr_0a_v(const FastSrc& s, uint32_t lo, uint32_t
   return (w & 0xffu) == 0x0au && (h < 4u || b3 < 0x80u) && bo + bl == lo + ll;
 }
 
-// Packed int64 lists of at least this many bytes are decoded by the whole wave (one byte per lane,
-// ~100 VALU per 64 bytes); shorter ones by their own lane (~40 VALU per value, all lanes in
-// parallel), which is cheaper when the record has many short lists (2.4 vs 3.3 ms).
-constexpr uint32_t kCoopIntBytes = 256;
+// Terminator bytes (< 0x80) among stage bytes [x0, x1) at stage offset `base`.
+__device__ __forceinline__ uint32_t count_terms(const uint8_t* l, uint32_t base, uint32_t x0, uint32_t x1) {
+  uint32_t n = 0;
+  for (uint32_t q = x0; q < x1; q += 4) {
+    uint32_t t = ~lds_u32u(l, base + q) & 0x80808080u;
+    if (x1 - q < 4u) t &= bytes_mask(x1 - q);
+    n += (uint32_t)__popc(t);
+  }
+  return n;
+}
+
+// One varint of 1..10 bytes at payload offset `pos`, branch-free: three word reads, the first
+// terminator by bit scan, the 7-bit groups of each word compacted under a byte mask and combined
+// (COMPAT: the reference's int-width shifts, decoder.pyx:34-50, as in fast_value). The caller
+// guarantees a terminator before the end of the body (its last byte is one), so the bytes read past
+// it never matter. false = more than 10 bytes (the exact path reports it).
+template <bool COMPAT>
+__device__ __forceinline__ bool varint_bf(const FastSrc& s, uint32_t& pos, int64_t& val) {
+  const uint32_t w0 = s.u32(pos), w1 = s.u32(pos + 4u), w2 = s.u32(pos + 8u);
+  const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
+  const uint32_t nb = t0 ? (__builtin_ctz(t0) >> 3) + 1u
+                         : t1 ? (__builtin_ctz(t1) >> 3) + 5u : t2 ? (__builtin_ctz(t2) >> 3) + 9u : 0u;
+  const uint32_t x = vgroups(w0, bytes_mask(nb));
+  const uint32_t x1 = nb > 4u ? vgroups(w1, bytes_mask(nb - 4u)) : 0u;         // groups 4..7
+  const uint32_t x2 = nb > 8u ? vgroups(w2 & 0xffffu, bytes_mask(nb - 8u)) : 0u;  // groups 8..9
+  pos += nb;
+  if (COMPAT) {
+    const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
+    const bool neg = ((x1 >> 3) | (x2 >> 7)) & 1u;
+    val = (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
+  } else {
+    val = (int64_t)((uint64_t)x | ((uint64_t)x1 << 28) | ((uint64_t)x2 << 56));
+  }
+  return nb != 0u;
+}
+
+// Canonical packed int64 lists of one staged record, balanced over the whole wave. The bodies of
+// the eligible slots (iv: one canonical chunk whose last byte is a terminator, so its value starts
+// are exactly its c values), in slot order, form one virtual byte axis of T bytes cut into 64 equal
+// ranges; lane j decodes every value that STARTS in its range [a, b). Its first value's index is
+// the number of starts before a (wave scan of the per-lane start counts) minus the slot's value
+// base. Per-slot parameters are fetched by lane shuffles in wave-uniform loops. A lane-per-list
+// decode waits for the wave's longest list (C3: lists of U[0,64] values, half the lanes idle on
+// float slots); this one gives every lane ~T/64 bytes. false = some value did not decode (or the
+// start count disagrees with the counts): every eligible slot then takes the per-lane path, which
+// rewrites its whole range (stores here never leave [dst, dst + c)).
+template <bool COMPAT>
+__device__ __forceinline__ bool int64_balanced(const FastSrc& fs, const DevOut& o, bool iv, uint32_t bo, uint32_t bl,
+                                               uint32_t c, uint64_t dst, uint32_t lane) {
+  const uint32_t len = iv ? bl : 0u, cnt = iv ? c : 0u;
+  const uint32_t vend = wave_incl_scan_u32(len, lane);  // virtual end of slot k's body (lane k)
+  const uint32_t T = __builtin_amdgcn_readlane(vend, 63);
+  if (!T) return true;
+  const uint32_t cend = wave_incl_scan_u32(cnt, lane);
+  const uint32_t a = (uint32_t)(((uint64_t)lane * T) >> 6), b = (uint32_t)(((uint64_t)(lane + 1u) * T) >> 6);
+  uint32_t k0 = 0;  // first slot whose body ends after a (vend is non-decreasing)
+#pragma unroll
+  for (uint32_t s = 32; s; s >>= 1)
+    if ((uint32_t)__shfl((int)vend, (int)(k0 + s - 1u), 64) <= a) k0 += s;
+  // pass 1: value starts in [a, b): position p of a body starts a value iff p == 0 or p-1 is a terminator
+  uint32_t starts = 0, k = k0, x = a;
+  while (__ballot(x < b)) {
+    const uint32_t kk = k < 64u ? k : 63u;
+    const uint32_t ve = (uint32_t)__shfl((int)vend, (int)kk, 64), vl = (uint32_t)__shfl((int)len, (int)kk, 64);
+    const uint32_t ko = (uint32_t)__shfl((int)bo, (int)kk, 64);
+    if (x < b && ve > x) {
+      const uint32_t vb = ve - vl, pa = x - vb, pe = (b < ve ? b : ve) - vb;
+      starts += (pa == 0u) + count_terms(fs.l, fs.p + ko, pa ? pa - 1u : 0u, pe - 1u);
+      x = b < ve ? b : ve;
+    }
+    ++k;
+  }
+  const uint32_t incl = wave_incl_scan_u32(starts, lane);
+  if (__builtin_amdgcn_readlane(incl, 63) != __builtin_amdgcn_readlane(cend, 63)) return false;
+  // pass 2: decode the owned values
+  uint32_t g = incl - starts;  // value starts before a
+  bool bad = false;
+  bool first = true;
+  k = k0;
+  x = a;
+  while (__ballot(x < b)) {
+    const uint32_t kk = k < 64u ? k : 63u;
+    const uint32_t ve = (uint32_t)__shfl((int)vend, (int)kk, 64), vl = (uint32_t)__shfl((int)len, (int)kk, 64);
+    const uint32_t ko = (uint32_t)__shfl((int)bo, (int)kk, 64);
+    const uint32_t ce = (uint32_t)__shfl((int)cend, (int)kk, 64), cl = (uint32_t)__shfl((int)cnt, (int)kk, 64);
+    const uint32_t dlo = (uint32_t)__shfl((int)(uint32_t)dst, (int)kk, 64);
+    const uint32_t dhi = (uint32_t)__shfl((int)(uint32_t)(dst >> 32), (int)kk, 64);
+    if (x < b && ve > x) {
+      const uint32_t vb = ve - vl, pa = x - vb, pe = (b < ve ? b : ve) - vb;
+      const uint64_t dk = ((uint64_t)dhi << 32) | dlo;
+      uint32_t idx = first ? g - (ce - cl) : 0u;
+      first = false;
+      uint32_t pos = ko + pa;  // payload offset
+      if (pa) {                // skip to the first start: after the first terminator at >= pa - 1
+        const uint32_t q = ko + pa - 1u;
+        const uint32_t t0 = ~fs.u32(q) & 0x80808080u, t1 = ~fs.u32(q + 4u) & 0x80808080u;
+        const uint32_t t2 = ~fs.u32(q + 8u) & 0x80808080u;
+        const uint32_t nt = t0 ? (__builtin_ctz(t0) >> 3) : t1 ? 4u + (__builtin_ctz(t1) >> 3)
+                                                           : t2 ? 8u + (__builtin_ctz(t2) >> 3) : 12u;
+        bad |= nt >= 12u;
+        pos = q + nt + 1u;
+      }
+      const uint32_t pend = ko + pe;
+      const uint32_t lim = dk + cl <= o.cap_i64 ? cl : (dk < o.cap_i64 ? (uint32_t)(o.cap_i64 - dk) : 0u);
+      int64_t* out = o.i64 + dk;
+      while (pos < pend) {
+        int64_t v;
+        if (!varint_bf<COMPAT>(fs, pos, v)) {
+          bad = true;
+          break;
+        }
+        if (idx < lim) out[idx] = v;
+        ++idx;
+      }
+      x = b < ve ? b : ve;
+    }
+    ++k;
+  }
+  return !__ballot(bad);
+}
 
 template <bool COMPAT>
 __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevOut& o, bool present, uint32_t kind,
@@ -2212,45 +2329,14 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
       if (d + j < o.cap_f32) o.f32[d + j] = lds_u32u(fs.l, fs.p + b0 + 4u * j);
     }
   }
-  // long canonical packed int64 lists: 64 bytes per wave step, one byte per lane; a lane holding a
-  // terminator decodes the varint ending there (its start is the previous terminator + 1, from the
-  // ballot) and stores it at its index among the terminators. The chunk must end on a terminator
-  // and hold exactly the counted values, else that slot takes the per-lane path below (which
-  // rewrites the whole range; stores here never leave [dst, dst + cnt)).
-  const bool coop = packed && kind == TFRG_KIND_INT64 && bl >= kCoopIntBytes;
-  fail |= packed && kind == TFRG_KIND_INT64 && !coop;
-  m = __ballot(coop);
-  while (m) {
-    const int k = __builtin_ctzll(m);
-    m &= m - 1;
-    const uint32_t b0 = __builtin_amdgcn_readlane(bo, k), nb = __builtin_amdgcn_readlane(bl, k);
-    const uint32_t c = __builtin_amdgcn_readlane(cnt, k);
-    const uint64_t d = readlane_u64(dst, k);
-    const uint32_t e = b0 + nb;
-    uint32_t done = 0, vst = b0;
-    bool bad = false;
-    for (uint32_t w0 = 0; w0 < nb; w0 += 64) {
-      const uint32_t j = w0 + lane;
-      const bool in = j < nb;
-      const uint32_t b = in ? fs.l[fs.p + b0 + j] : 0x80u;
-      const bool t = !(b & 0x80u);
-      const uint64_t tm = __ballot(t);
-      const uint64_t below = tm & ((1ull << lane) - 1ull);
-      if (t) {
-        uint32_t pos = below ? b0 + w0 + 64u - (uint32_t)__builtin_clzll(below) : vst;
-        const uint32_t idx = done + (uint32_t)__popcll(below);
-        int64_t v;
-        const bool okv = fast_value<COMPAT>(fs, pos, e, v) && pos == b0 + j + 1u;
-        if (okv && idx < c && d + idx < o.cap_i64) o.i64[d + idx] = v;
-        bad |= !okv;
-      }
-      done += (uint32_t)__popcll(tm);
-      if (tm) vst = b0 + w0 + 64u - (uint32_t)__builtin_clzll(tm);
-    }
-    if (__ballot(bad) || done != c || vst != e) fail |= lane == (uint32_t)k;
-  }
+  PHASE_MARK(gf);
+  PHASE_ADD(15, g0, gf);
+  // canonical packed int64 lists: balanced over the whole wave
+  const bool iv = packed && kind == TFRG_KIND_INT64 && bl > 0u && fs.l[fs.p + bo + bl - 1u] < 0x80u;
+  fail |= packed && kind == TFRG_KIND_INT64 && !iv;
+  if (!int64_balanced<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane)) fail |= iv;
   PHASE_MARK(g1);
-  PHASE_ADD(11, g0, g1);
+  PHASE_ADD(11, gf, g1);
   if (present && (kind == TFRG_KIND_BYTES || fail)) {
     if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst)) {
       LdsSrc s;

@@ -68,7 +68,7 @@ def main():
         arr = (ctypes.c_ulonglong * 32)()
         L.tfrg_debug_phase(arr, 32, 1)
         names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
-                 "c.bails", "g.stage+meta", "g.groups", "g.float", "g.lane", "h.crc", "h.walk", "-",
+                 "c.bails", "g.stage+meta", "g.groups", "g.int64", "g.lane", "h.crc", "h.walk", "g.float",
                  "l.span+stage", "l.crc", "l.walk", "l.final", "l.total"]
         tot = (arr[20] or arr[7]) or 1
         for i, nm in enumerate(names):
