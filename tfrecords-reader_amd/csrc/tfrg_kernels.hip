@@ -662,7 +662,7 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
 #ifndef TFRG_LANE_MINB
-#define TFRG_LANE_MINB 4  // workgroups per CU the count kernel is register-budgeted for
+#define TFRG_LANE_MINB 6  // workgroups per CU the count kernel is register-budgeted for (dict in LDS)
 #endif
 constexpr int kWaveBlock = 256;
 constexpr int kWavesPerBlock = kWaveBlock / 64;
@@ -864,17 +864,45 @@ struct FastSrc {
   __device__ __forceinline__ uint32_t w4s(uint32_t i) const { return i < L ? w4(i) : 0u; }
   // 4 bytes at payload offset i, unmasked (the canonical walker bounds-checks what it uses)
   __device__ __forceinline__ uint32_t u32(uint32_t i) const { return lds_u32u(l, p + i); }
+  __device__ __forceinline__ void window(uint32_t) const {}  // (the stage is the window)
 };
 
 // The same payload view over HBM (records beyond the LDS stage): two aligned dword loads + a byte
 // funnel shift, clamped to the readable end of the batch (round_up(nbytes, 16)).
+// A 32-byte register window (two aligned 16-byte blocks) is loaded at the start of every map entry
+// (window()): the entry's headers, a short key and the first list chunk header are then served
+// from registers, one HBM round trip per entry instead of one per dependent header.
 struct FastSrcG {
   const uint8_t* buf;
   uint64_t base;  // absolute payload start
   uint32_t L;
   uint64_t lim;   // last readable dword
+  mutable uint64_t wa = 0;  // window start (16-aligned absolute address)
+  mutable bool wv = false;  // window loaded
+  mutable uint4 b0, b1;
+  __device__ __forceinline__ void window(uint32_t i) const {
+    const uint64_t a = (base + i) & ~15ull;
+    wv = a + 32u <= lim + 4u;  // both blocks readable
+    const uint64_t lb = lim - 12u;  // last readable 16-byte block
+    wa = a;
+    b0 = *reinterpret_cast<const uint4*>(buf + (a < lb ? a : lb));
+    b1 = *reinterpret_cast<const uint4*>(buf + (a + 16u < lb ? a + 16u : lb));
+  }
   __device__ __forceinline__ uint32_t u32(uint32_t i) const {
-    const uint64_t a = base + i, a0 = a & ~3ull;
+    const uint64_t a = base + i;
+    const uint64_t off = a - wa;
+    if (wv && off <= 27u) {  // words k, k+1 of the window: select chains (no dynamic register index)
+      const uint32_t k = (uint32_t)off >> 2;
+      const uint32_t e0 = (k & 1u) ? b0.y : b0.x, e1 = (k & 1u) ? b0.w : b0.z;
+      const uint32_t e2 = (k & 1u) ? b1.y : b1.x, e3 = (k & 1u) ? b1.w : b1.z;
+      const uint32_t lo = k < 4u ? ((k & 2u) ? e1 : e0) : ((k & 2u) ? e3 : e2);
+      const uint32_t k1 = k + 1u;
+      const uint32_t f0 = (k1 & 1u) ? b0.y : b0.x, f1 = (k1 & 1u) ? b0.w : b0.z;
+      const uint32_t f2 = (k1 & 1u) ? b1.y : b1.x, f3 = (k1 & 1u) ? b1.w : b1.z;
+      const uint32_t hi = k1 < 4u ? ((k1 & 2u) ? f1 : f0) : ((k1 & 2u) ? f3 : f2);
+      return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(a & 3u));
+    }
+    const uint64_t a0 = a & ~3ull;
     const uint32_t w0 = *reinterpret_cast<const uint32_t*>(buf + (a0 < lim ? a0 : lim));
     const uint32_t w1 = *reinterpret_cast<const uint32_t*>(buf + (a0 + 4 < lim ? a0 + 4 : lim));
     return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(a & 3u));
@@ -1173,6 +1201,7 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
   const uint32_t fe = fo + fl;
   for (uint32_t q = fo; ok && q < fe;) {
     uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
+    s.window(q);
     ok = hdr2(s, q, fe, en, eo, el) & (en == 1u);
     const uint32_t ee = eo + el;
     q = ee;
@@ -1320,7 +1349,8 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
 // MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
 template <int R, bool COMPAT, int MODE>
-__global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4)
+    void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
