@@ -662,7 +662,7 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
 #ifndef TFRG_LANE_MINB
-#define TFRG_LANE_MINB 6  // workgroups per CU the count kernel is register-budgeted for (dict in LDS)
+#define TFRG_LANE_MINB 4  // workgroups per CU the count kernel is register-budgeted for
 #endif
 constexpr int kWaveBlock = 256;
 constexpr int kWavesPerBlock = kWaveBlock / 64;
@@ -871,7 +871,9 @@ struct FastSrc {
 // funnel shift, clamped to the readable end of the batch (round_up(nbytes, 16)).
 // A 32-byte register window (two aligned 16-byte blocks) is loaded at the start of every map entry
 // (window()): the entry's headers, a short key and the first list chunk header are then served
-// from registers, one HBM round trip per entry instead of one per dependent header.
+// from registers, one HBM round trip per entry instead of one per dependent header. WIN = false
+// compiles the window out (the per-lane-dict kernel: its registers would cost C1 occupancy).
+template <bool WIN>
 struct FastSrcG {
   const uint8_t* buf;
   uint64_t base;  // absolute payload start
@@ -881,6 +883,7 @@ struct FastSrcG {
   mutable bool wv = false;  // window loaded
   mutable uint4 b0, b1;
   __device__ __forceinline__ void window(uint32_t i) const {
+    if (!WIN) return;
     const uint64_t a = (base + i) & ~15ull;
     wv = a + 32u <= lim + 4u;  // both blocks readable
     const uint64_t lb = lim - 12u;  // last readable 16-byte block
@@ -891,7 +894,7 @@ struct FastSrcG {
   __device__ __forceinline__ uint32_t u32(uint32_t i) const {
     const uint64_t a = base + i;
     const uint64_t off = a - wa;
-    if (wv && off <= 27u) {  // words k, k+1 of the window: select chains (no dynamic register index)
+    if (WIN && wv && off <= 27u) {  // words k, k+1 of the window: select chains (no dynamic register index)
       const uint32_t k = (uint32_t)off >> 2;
       const uint32_t e0 = (k & 1u) ? b0.y : b0.x, e1 = (k & 1u) ? b0.w : b0.z;
       const uint32_t e2 = (k & 1u) ? b1.y : b1.x, e3 = (k & 1u) ? b1.w : b1.z;
@@ -995,7 +998,8 @@ __device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e,
 // count_packed over HBM (records walked from HBM): aligned 16-byte blocks, two loads in flight per
 // round instead of one dependent dword pair per word (a packed list of 300 bytes was 75 serial
 // round trips; four blocks per round would cost the staged path its occupancy in VGPRs)
-__device__ __forceinline__ bool count_packed(const FastSrcG& s, uint32_t o, uint32_t e, uint32_t& cnt) {
+template <bool WIN>
+__device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o, uint32_t e, uint32_t& cnt) {
   uint32_t run = 0, terms = 0;
   const uint64_t a0 = s.base + o, a1 = s.base + e;
   const uint64_t lb = s.lim - 12;  // last readable 16-byte block
@@ -1349,8 +1353,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
 // MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
 template <int R, bool COMPAT, int MODE>
-__global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4)
-    void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1461,7 +1464,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4)
       if (bigw) {
         frame_verdicts<R, false>(B, v, T, nullptr, 0, mine);
         sink.fast_reset(S);
-        const FastSrcG fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
+        const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
         done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
         tried = true;
       }
