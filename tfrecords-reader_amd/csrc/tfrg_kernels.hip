@@ -2513,11 +2513,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageSlowCount);
+  // the exception paths (slow records, out-of-line lane lists) are usually empty: a grid of two
+  // workgroups per CU (grid-stride loops) keeps their dispatch cheap
+  const uint32_t tail_grid = (uint32_t)cfg.lane_grid < 2u * (uint32_t)cfg.num_cus ? (uint32_t)cfg.lane_grid
+                                                                                   : 2u * (uint32_t)cfg.num_cus;
   if (slow_lds <= kLaneLdsBudget) {
-    hipLaunchKernelGGL((k_slow_count<1, COMPAT, false>), dim3(cfg.lane_grid), dim3(kLaneBlock), slow_lds, st, b, sc,
+    hipLaunchKernelGGL((k_slow_count<1, COMPAT, false>), dim3(tail_grid), dim3(kLaneBlock), slow_lds, st, b, sc,
                        o, d_tab, cfg.lane_max);
   } else {
-    hipLaunchKernelGGL((k_slow_count<1, COMPAT, true>), dim3(cfg.lane_grid), dim3(kLaneBlock), 2048ull * 4, st, b,
+    hipLaunchKernelGGL((k_slow_count<1, COMPAT, true>), dim3(tail_grid), dim3(kLaneBlock), 2048ull * 4, st, b,
                        sc, o, d_tab, cfg.lane_max);
   }
   mark(kStageWaveCount);
@@ -2539,7 +2543,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   }
   mark(kStageListGather);
   if (S > 0)
-    hipLaunchKernelGGL((k_list_gather<COMPAT>), dim3(cfg.lane_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
+    hipLaunchKernelGGL((k_list_gather<COMPAT>), dim3(tail_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
                        cfg.lane_max);
   mark(kStageWaveGather);
   if (S > 0) {
