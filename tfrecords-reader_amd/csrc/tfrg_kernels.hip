@@ -2231,20 +2231,28 @@ __device__ __forceinline__ uint32_t count_terms(const uint8_t* l, uint32_t base,
   return n;
 }
 
-// One varint of 1..10 bytes at payload offset `pos`, branch-free: three word reads, the first
-// terminator by bit scan, the 7-bit groups of each word compacted under a byte mask and combined
+// One varint of 1..10 bytes at payload offset `pos`, branch-free: four aligned dwords give the 12
+// bytes at pos, per-word masks of the bytes up to the first terminator give its length (popcount),
+// the 7-bit groups of each word are compacted under those masks and combined
 // (COMPAT: the reference's int-width shifts, decoder.pyx:34-50, as in fast_value). The caller
 // guarantees a terminator before the end of the body (its last byte is one), so the bytes read past
 // it never matter. false = more than 10 bytes (the exact path reports it).
 template <bool COMPAT>
 __device__ __forceinline__ bool varint_bf(const FastSrc& s, uint32_t& pos, int64_t& val) {
-  const uint32_t w0 = s.u32(pos), w1 = s.u32(pos + 4u), w2 = s.u32(pos + 8u);
+  // four aligned dwords (two ds_read2 from one address) -> the 12 bytes at pos
+  const uint32_t off = s.p + pos, sh = off & 3u;
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(s.l) + (off >> 2);
+  const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
   const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
-  const uint32_t nb = t0 ? (__builtin_ctz(t0) >> 3) + 1u
-                         : t1 ? (__builtin_ctz(t1) >> 3) + 5u : t2 ? (__builtin_ctz(t2) >> 3) + 9u : 0u;
-  const uint32_t x = vgroups(w0, bytes_mask(nb));
-  const uint32_t x1 = nb > 4u ? vgroups(w1, bytes_mask(nb - 4u)) : 0u;         // groups 4..7
-  const uint32_t x2 = nb > 8u ? vgroups(w2 & 0xffffu, bytes_mask(nb - 8u)) : 0u;  // groups 8..9
+  // per word, the bits of the bytes up to and including the first terminator (t ^ (t - 1): all
+  // ones when the word has none; zero past the terminator's word) -- selects, no branches
+  const uint32_t m0 = t0 ^ (t0 - 1u);
+  const uint32_t m1 = t0 ? 0u : t1 ^ (t1 - 1u);
+  const uint32_t m2 = (t0 | t1) ? 0u : (t2 ^ (t2 - 1u)) & 0xffffu;
+  const uint32_t nb = (uint32_t)(__popc(m0) + __popc(m1) + __popc(m2)) >> 3;
+  const uint32_t x = vgroups(w0, m0), x1 = vgroups(w1, m1), x2 = vgroups(w2, m2);  // groups 0-3, 4-7, 8-9
   pos += nb;
   if (COMPAT) {
     const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
@@ -2253,7 +2261,7 @@ __device__ __forceinline__ bool varint_bf(const FastSrc& s, uint32_t& pos, int64
   } else {
     val = (int64_t)((uint64_t)x | ((uint64_t)x1 << 28) | ((uint64_t)x2 << 56));
   }
-  return nb != 0u;
+  return (t0 | t1 | t2) != 0u;  // else more than 10 bytes
 }
 
 // Canonical packed int64 lists of one staged record, balanced over the whole wave. The bodies of
@@ -2325,12 +2333,9 @@ __device__ __forceinline__ bool int64_balanced(const FastSrc& fs, const DevOut& 
       const uint32_t pend = ko + pe;
       const uint32_t lim = dk + cl <= o.cap_i64 ? cl : (dk < o.cap_i64 ? (uint32_t)(o.cap_i64 - dk) : 0u);
       int64_t* out = o.i64 + dk;
-      while (pos < pend) {
+      while (pos < pend) {  // (a failed varint still advances: the slot is redone per lane)
         int64_t v;
-        if (!varint_bf<COMPAT>(fs, pos, v)) {
-          bad = true;
-          break;
-        }
+        bad |= !varint_bf<COMPAT>(fs, pos, v);
         if (idx < lim) out[idx] = v;
         ++idx;
       }
