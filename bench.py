@@ -1,17 +1,23 @@
 #!/usr/bin/env python3
 """Device-resident TFRecord -> tf.train.Example -> Feature decode throughput on MI355X.
 
-Workload (BASELINE.json configs[1], C1, scaled for a rate measurement as SURVEY §8d D3 asks): per
-GPU one resident batch of 256 files x 65,536 C1-shaped records (int64 label + 12-byte bytes_list
-id, ~59 B framed, spec CRC-32C) = 16,777,216 records, ~0.92 GiB. A step is one full decode of that
-batch: framing check + masked CRC-32C of length and payload + reference-exact Example decode +
-columnar gather of every value (k_lane_count .. k_wave_gather), inputs already in HBM. At N GPUs
-every rank decodes its own 256-file shard (weak scaling, no collective on the data path; the
-barrier and the max-over-ranks timing use RCCL).
+Headline workload (BASELINE.json configs[4] with configs[1]'s record shape): a
+directory of 32 x N TFRecord files for N GPUs (N = 8: the 256-file C4 directory). File f holds
+C1-shaped records (int64 label + 12-byte bytes_list id, ~59 B framed, spec CRC-32C); its record
+count is drawn from default_rng(1000 + f), uniform in +-50 % around 2^19 (~29 MiB per file). The
+files are partitioned over the ranks by LPT on bytes (tfr_reader/shard.py), each rank indexes its
+own files with the native framing indexer and decodes them as ONE resident batch (~0.92 GiB,
+~16.8 M records per GPU): weak scaling, no collective on the data path. A step is one full decode
+of that batch (framing check + masked CRC-32C of length and payload + reference-exact Example
+decode + columnar gather of every value), inputs already in HBM.
 
-Prints ONE JSON line (rank 0). ``roofline`` is for the dominant kernel, timed with HIP events on
-the stream the kernels run on; ``cpu_baseline`` is the oracle (the C restatement of the reference
-decoder) on host threads over a bounded sample of the same records.
+``python bench.py --gpus N`` spawns N ranks itself (before any GPU call) when it is not launched by
+torch.distributed.run; under torchrun it reads RANK / LOCAL_RANK / WORLD_SIZE. RCCL carries only the
+barrier and the max-over-ranks time and byte sums.
+
+At N = 1 the same run also measures the other configs under ``configs`` (one resident 65,536-record
+C1 file, C2 flowers-shaped records, C3 wide-schema records, the C2-shaped C4 directory), each with
+its own roofline and CPU baseline. Prints ONE JSON line (rank 0).
 """
 
 from __future__ import annotations
@@ -19,6 +25,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
 import sys
 import time
 from concurrent.futures import ThreadPoolExecutor
@@ -33,171 +40,221 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E peak, 8.0 TB/s (MI355X_MICROARCH.md, chip-level parameters)
-RECORDS_PER_FILE = 65536
-FILES_PER_GPU = 256
+FILES_PER_GPU = 32
 
 
-def parse_args():
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"],
-                    help="c1 (default, configs[1]); c2 flowers-shaped; c3 wide schema")
-    ap.add_argument("--files", type=int, default=None, help="replicas of the base file per GPU")
+    ap.add_argument("--files-per-gpu", type=int, default=FILES_PER_GPU)
+    ap.add_argument("--only", default=None, choices=["c4", "c1file", "c2", "c3", "c4c2"],
+                    help="measure one config only and report it as the headline (profiling runs)")
+    ap.add_argument("--no-extra", action="store_true", help="skip the per-config measurements at N = 1")
     ap.add_argument("--profile-steps", type=int, default=5)
-    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of the CPU baseline")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of each CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-CONFIGS = {
-    # name: (default replicas of the base file per GPU, description)
-    "c1": (FILES_PER_GPU, "C1 (configs[1]): {files} files x 65536 records per GPU, int64 label + 12 B bytes_list id"),
-    "c2": (1, "C2 (configs[2]): oxford_flowers102-shaped, {files} x 8189 records per GPU, lognormal image bytes"),
-    "c3": (16, "C3 (configs[3]): wide schema 32 int64_list + 32 float_list, {files} x 8192 records per GPU"),
-}
+# ------------------------------------------------------------------------------------------------
+# workloads
+# ------------------------------------------------------------------------------------------------
+class Workload:
+    """One resident batch: framed bytes + absolute (start, end) + the record groups ("files") the
+    CPU baseline distributes over host cores."""
+
+    def __init__(self, name: str, desc: str, buf, starts, ends, units) -> None:
+        self.name, self.desc = name, desc
+        self.buf, self.starts, self.ends = buf, starts, ends
+        self.units = units  # [(first record, end record)]
+
+    @property
+    def n(self) -> int:
+        return int(self.starts.shape[0])
+
+    @property
+    def framed_bytes(self) -> int:
+        return int((self.ends - self.starts).sum())
 
 
-def base_payloads(config: str, rank: int) -> list[bytes]:
+def _gen(fn, items, threads=8):
+    with ThreadPoolExecutor(threads) as ex:
+        return list(ex.map(fn, items))
+
+
+def c4_workload(shape: str, rank: int, world: int, files_per_gpu: int):
+    from tfr_reader import shard, synth
+
+    n_files = files_per_gpu * world
+    sizes = synth.c4_file_sizes(n_files, shape)
+    parts = shard.lpt_partition(sizes, world)
+    mine = parts[rank]
+    imgs = _gen(lambda f: synth.c4_file(f, shape), mine)
+    sb = shard.ShardBatch([synth.c4_file_name(f) for f in mine], imgs)
+    loads = np.array([sizes[p].sum() for p in parts], np.float64)
+    units = [(int(sb.file_first[i]), int(sb.file_first[i + 1])) for i in range(len(mine))]
+    base = synth.C4_C1_BASE if shape == "c1" else synth.C4_C2_BASE
+    rec = "C1-shaped (int64 label + 12 B bytes_list id)" if shape == "c1" else \
+        "C2-shaped (flowers: lognormal image bytes_list + int64 label + file_name)"
+    desc = (f"C4 directory (configs[4]) of {n_files} files ({files_per_gpu} per GPU, LPT by bytes), {rec} "
+            f"records, {base} +-50 % per file (default_rng(1000+f)), spec CRC-32C, resident in HBM")
+    w = Workload(f"c4_{shape}", desc, sb.buf, sb.starts, sb.ends, units)
+    w.files_total, w.files_mine = n_files, len(mine)
+    w.lpt_max_over_mean = float(loads.max() / loads.mean())
+    return w
+
+
+def single_workload(name: str) -> Workload:
     from tfr_reader import synth
 
-    if config == "c1":
-        return synth.c1_payloads(RECORDS_PER_FILE, offset=rank * RECORDS_PER_FILE)
-    if config == "c2":
-        return synth.c2_payloads(8189, seed=2 + rank)
-    return synth.c3_payloads(8192, seed=3 + rank)
+    if name == "c1file":
+        blob, offs = synth.c1_blob(65536)
+        buf = synth.frame_blob(blob, offs)
+        lens = np.diff(offs) + 16
+        en = np.cumsum(lens, dtype=np.uint64)
+        st = en - lens
+        desc = "C1 (configs[1]): one file of 65,536 C1-shaped records (3.7 MiB) resident, one decode per step"
+        return Workload(name, desc, buf, st, en, [(0, 65536)])
+    if name == "c2":
+        buf, st, en = synth.framed(synth.c2_payloads(8189, seed=2))
+        desc = "C2 (configs[2]): 8,189 oxford_flowers102-shaped records (lognormal image bytes, median 40 KiB)"
+        return Workload(name, desc, buf, st, en, [(i, min(i + 256, 8189)) for i in range(0, 8189, 256)])
+    base = synth.framed(synth.c3_payloads(8192, seed=3))
+    buf, st, en = synth.replicate(*base, 16)
+    desc = "C3 (configs[3]): 16 x 8,192 wide-schema records (32 int64_list + 32 float_list, U[0,64] values)"
+    return Workload(name, desc, buf, st, en, [(i, i + 512) for i in range(0, 16 * 8192, 512)])
 
 
-def build_shard(rank: int, config: str, files: int):
-    """Framed base file (seeded by rank) replicated `files` times."""
-    from tfr_reader import synth
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (C restatement of the reference decoder) on the host cores
+# ------------------------------------------------------------------------------------------------
+def host_cores() -> dict:
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_cpus": quota, "threads": min(aff, quota) if quota else aff}
 
-    pl = base_payloads(config, rank)
-    buf, st, en = synth.framed(pl, crc=True)
-    return (buf, st, en), synth.replicate(buf, st, en, files)
 
-
-def cpu_baseline(sample, seconds: float, config: str = "c1") -> dict:
-    """Oracle decode (restated reference algorithm, C) of the sample on host threads."""
+def cpu_baseline(w: Workload, seconds: float) -> dict:
+    """Units (files / record groups) of the workload spread over one worker thread per host core;
+    each worker decodes whole units round-robin until the wall budget is spent (bounded sample)."""
     from oracle import oracle as O
 
-    buf, st, en = sample
     O.lib()
-    cores = min(16, len(os.sched_getaffinity(0)))
-    nbytes = int((en - st).sum())
+    hc = host_cores()
+    T = hc["threads"]
+    buf = w.buf
 
-    def work(_):
+    def work(t):
+        mine = w.units[t::T] or [w.units[t % len(w.units)]]
         done_b = done_r = 0
         t0 = time.perf_counter()
+        k = 0
         while time.perf_counter() - t0 < seconds:
-            status, _ = O.decode_framed_bulk(buf, st, en)
+            lo, hi = mine[k % len(mine)]
+            status, _ = O.decode_framed_bulk(buf, w.starts[lo:hi], w.ends[lo:hi])
             assert not status.any()
-            done_b += nbytes
-            done_r += st.shape[0]
+            done_b += int((w.ends[lo:hi] - w.starts[lo:hi]).sum())
+            done_r += hi - lo
+            k += 1
         return done_b, done_r
 
     t0 = time.perf_counter()
-    with ThreadPoolExecutor(cores) as ex:
-        res = list(ex.map(work, range(cores)))
+    with ThreadPoolExecutor(T) as ex:
+        res = list(ex.map(work, range(T)))
     wall = time.perf_counter() - t0
     b = sum(r[0] for r in res)
     r = sum(r[1] for r in res)
     return {
-        "value": b / wall / 2**30,
+        "value": round(b / wall / 2**30, 3),
         "unit": "GiB/s",
-        "examples_per_s": r / wall,
-        "cores": cores,
+        "examples_per_s": round(r / wall, 1),
+        "cores": T,
+        "host_cpus": hc,
         "kind": "port",
-        "sample": f"one {config.upper()} file ({st.shape[0]} records, {nbytes / 2**20:.2f} MiB) decoded repeatedly by "
-        f"{cores} threads for {seconds:.1f} s wall ({cores * seconds:.0f} core-s)",
+        "sample": f"{w.name}: its {len(w.units)} files / record groups spread over {T} threads (one per "
+        f"host core), each decoding whole units (CRC-32C verdicts + reference decode) for "
+        f"{seconds:.1f} s wall ({T * seconds:.0f} core-s); {r} records decoded",
     }
 
 
-def main() -> None:
-    args = parse_args()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    # TFRG_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
-    # devices round-robin); the driver's runs use RCCL ("nccl"), one rank per GPU
-    backend = os.environ.get("TFRG_BENCH_BACKEND", "nccl")
-    if backend != "nccl":
-        local = local % max(1, torch.cuda.device_count())
-    if dist:
-        import torch.distributed as tdist
+# ------------------------------------------------------------------------------------------------
+# device measurement
+# ------------------------------------------------------------------------------------------------
+class Ctx:
+    def __init__(self, dev, stream, dec, dist, backend):
+        self.dev, self.stream, self.dec, self.dist, self.backend = dev, stream, dec, dist, backend
 
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        if backend == "nccl":
-            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
-        else:
-            tdist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(local)
 
+def _learn_schema(ctx: Ctx, w: Workload) -> None:
+    k = min(w.n, 4096)
+    lo, hi = int(w.starts[0]), int(w.ends[k - 1])
+    ctx.dec.decode(w.buf[lo:hi], w.starts[:k] - lo, w.ends[:k] - lo)
+
+
+def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> dict:
     from tfr_reader import hip
 
-    files = args.files if args.files is not None else CONFIGS[args.config][0]
-    sample, (big, st, en) = build_shard(rank, args.config, files)
-    n = int(st.shape[0])
-    nbytes = int(big.size)
-    framed_bytes = int((en - st).sum())
-    dev = torch.device("cuda", local)
+    dec, dev, stream = ctx.dec, ctx.dev, ctx.stream
+    nbytes = int(w.buf.size)
     d_bytes = torch.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
-    d_bytes[:nbytes].copy_(torch.from_numpy(big))
-    d_st = torch.from_numpy(st.view(np.int64)).to(dev)
-    d_en = torch.from_numpy(en.view(np.int64)).to(dev)
-    del big
-    # a dedicated stream: torch's default stream has handle 0, which the C-ABI reads as "use the
-    # context's own stream", and events recorded on it would not bracket the decode
-    stream = torch.cuda.Stream(dev)
-
-    dec = hip.HipDecoder(local)
-    res0 = dec.decode(*sample)  # learns the key table (host path, schema-miss rounds)
-    present_per_rec = float((res0.order != 0).sum()) / max(1, int(sample[1].shape[0]))
+    d_bytes[:nbytes].copy_(torch.from_numpy(w.buf))
+    d_st = torch.from_numpy(w.starts.view(np.int64)).to(dev)
+    d_en = torch.from_numpy(w.ends.view(np.int64)).to(dev)
+    n = w.n
+    _learn_schema(ctx, w)
 
     def step():
         dec.decode_device(d_bytes.data_ptr(), nbytes, d_st.data_ptr(), d_en.data_ptr(), n, stream=stream.cuda_stream)
 
-    for _ in range(args.warmup):
+    for _ in range(max(1, warmup)):
         step()
     torch.cuda.synchronize(dev)
     info = dec.info()
+    if info.n_miss_records:  # keys beyond the sample: learn them from the whole batch, warm up again
+        dec.decode(w.buf, w.starts, w.ends)
+        for _ in range(max(1, warmup)):
+            step()
+        info = dec.info()
     assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0, "decode check failed"
-    if args.config == "c1":
-        assert info.kind_totals[3] == n and info.kind_totals[1] == n, "value totals"
 
-    # ---- timed region
-    if dist:
+    # ---- timed region: barrier + synchronize on both sides, max over ranks
+    if ctx.dist:
+        import torch.distributed as tdist
+
         tdist.barrier()
     torch.cuda.synchronize(dev)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     e0.record(stream)
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
     e1.record(stream)
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    if dist:
+    if ctx.dist:
         tdist.barrier()
-    ev_s = e0.elapsed_time(e1) / 1e3
-    elapsed = max(wall, ev_s)
-    cdev = dev if backend == "nccl" else torch.device("cpu")  # collective tensors
-    if dist:
+    elapsed = max(wall, e0.elapsed_time(e1) / 1e3)
+    if ctx.dist:
+        cdev = dev if ctx.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
     info = dec.info()
     assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0
 
-    # ---- per-kernel durations (HIP events on the launch stream), for the roofline
+    # ---- per-kernel durations: HIP events recorded by libtfrg on the launch stream
     dec.set_profiling(True)
     per: dict[str, list[float]] = {}
-    for _ in range(args.profile_steps):
+    for _ in range(prof_steps):
         step()
         for k, v in dec.profile_last().items():
             per.setdefault(k, []).append(v)
@@ -205,22 +262,19 @@ def main() -> None:
     kern_ms = {k: float(np.mean(v)) for k, v in per.items()}
     dominant = max(kern_ms, key=kern_ms.get)
 
-    # algorithmic bytes per launch: the compulsory HBM traffic of each kernel.
-    # Lane count: every framed byte of its records + the two u64 offsets, status (4 B) + verdict
-    # (1 B) + order/count (2 + 4 B per slot) + one loc word (8 B) per present list. Wave count: the
-    # framed bytes + offsets. Down-gather: counts read, row splits written (4 + 4 B per slot and
-    # record), every value written (8 B int64 / 4 B float / 8 B bytes view) and the loc word it comes
-    # from when inline. Spine: tile sums read + written.
+    # algorithmic bytes per launch: the compulsory HBM traffic of each kernel
     n_slots = len(dec.keys.slot_key)
     n_big = int(info.n_big)
-    sz = en - st
-    big_sel = sz > hip.DEFAULT_LANE_MAX
-    big_bytes = int(sz[big_sel].sum())
-    small_bytes = framed_bytes - big_bytes
+    sz = w.ends - w.starts
+    big_bytes = int(sz[sz > hip.DEFAULT_LANE_MAX].sum())
+    framed = w.framed_bytes
+    small_bytes = framed - big_bytes
     n_small = n - n_big
-    present_small = int(present_per_rec * n_small)
-    n_vals = int(info.kind_totals[3]) + int(info.kind_totals[2]) + int(info.kind_totals[1])
-    vals = 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 8 * int(info.kind_totals[1])
+    kt = info.kind_totals
+    n_vals = int(kt[3]) + int(kt[2]) + int(kt[1])
+    vals = 8 * int(kt[3]) + 4 * int(kt[2]) + 8 * int(kt[1])
+    present = _present_lists(dec, w)
+    present_small = int(present * n_small / max(n, 1))
     n_tiles = (n + 255) // 256
     alg = {
         "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
@@ -231,88 +285,170 @@ def main() -> None:
         "k_list_gather": vals,
         "k_wave_gather": vals,
     }
-    a_bytes = alg.get(dominant, framed_bytes + 20 * n)
+    a_bytes = alg.get(dominant, framed + 20 * n)
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
-    # whole-pipeline algorithmic bytes: R + W
     n_keys = len(dec.keys.keys)
-    R = framed_bytes + 16 * n
-    W = 4 * n + 4 * n * n_keys + 8 * int(info.kind_totals[3]) + 4 * int(info.kind_totals[2]) + 12 * int(info.kind_totals[1])
+    R = framed + 16 * n
+    W = 4 * n + 4 * n * n_keys + 8 * int(kt[3]) + 4 * int(kt[2]) + 12 * int(kt[1])
+    ms_step = elapsed / steps * 1e3
+    out = {
+        "workload": w.desc,
+        "records": n,
+        "framed_bytes": framed,
+        "ms_per_step": round(ms_step, 4),
+        "GiB_s": round(framed / (ms_step / 1e3) / 2**30, 3),
+        "examples_per_s": round(n / (ms_step / 1e3), 1),
+        "kernels_ms": {k: round(v, 4) for k, v in kern_ms.items()},
+        "roofline": {
+            "kernel": dominant,
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / PEAK_HBM_GBS, 4),
+            "traffic": None,
+            "algorithmic_bytes_per_launch": a_bytes,
+        },
+        "pipeline": {
+            "alg_bytes_R_plus_W": R + W,
+            "achieved_GBps": round((R + W) / (ms_step / 1e3) / 1e9, 1),
+            "frac": round((R + W) / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
+        },
+        "_elapsed": elapsed,
+        "_d_bytes": d_bytes,
+    }
+    traffic = _traffic(w.name, dominant)
+    if traffic:
+        out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic
+    return out
 
-    # ---- achievable HBM read bandwidth on this box: streaming read of the batch
+
+def _present_lists(dec, w: Workload) -> float:
+    """Present (key, kind) lists over the batch, estimated from the schema sample decode."""
+    k = min(w.n, 4096)
+    lo, hi = int(w.starts[0]), int(w.ends[k - 1])
+    r = dec.decode(w.buf[lo:hi], w.starts[:k] - lo, w.ends[:k] - lo)
+    return float((r.order != 0).sum()) * w.n / k
+
+
+def _traffic(name: str, kernel: str):
+    """HBM bytes per launch of the dominant kernel from the committed PMC passes of this workload
+    (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), else None."""
+    tf = REPO / "profiles" / f"traffic_{name}.json"
+    if not tf.is_file():
+        return None
+    t = json.loads(tf.read_text())
+    if kernel not in t.get("kernel", ""):
+        return None
+    return int(t["traffic_bytes"]), f"profiles/{tf.name}"
+
+
+def stream_read_gbs(ctx: Ctx, d_bytes) -> float:
+    """Achievable HBM read bandwidth on this box: streaming read of the batch."""
     from tfr_reader import _native
 
     L = _native.lib()
-    sink = torch.zeros(4, dtype=torch.int32, device=dev)
-    rd_bytes = (nbytes // 16) * 16
+    sink = torch.zeros(4, dtype=torch.int32, device=ctx.dev)
+    rd = (int(d_bytes.numel()) // 16) * 16
 
-    def stream_read():
-        _native.check(L.tfrg_stream_read(d_bytes.data_ptr(), rd_bytes, sink.data_ptr(), stream.cuda_stream),
+    def go():
+        _native.check(L.tfrg_stream_read(d_bytes.data_ptr(), rd, sink.data_ptr(), ctx.stream.cuda_stream),
                       "tfrg_stream_read")
 
     for _ in range(3):
-        stream_read()
+        go()
     s0 = torch.cuda.Event(enable_timing=True)
     s1 = torch.cuda.Event(enable_timing=True)
-    s0.record(stream)
+    s0.record(ctx.stream)
     for _ in range(10):
-        stream_read()
-    s1.record(stream)
-    torch.cuda.synchronize(dev)
-    hbm_read_gbs = rd_bytes * 10 / (s0.elapsed_time(s1) / 1e3) / 1e9
+        go()
+    s1.record(ctx.stream)
+    torch.cuda.synchronize(ctx.dev)
+    return rd * 10 / (s0.elapsed_time(s1) / 1e3) / 1e9
 
-    # ---- single-batch figure: one base file resident, one decode, HIP events
-    sb_buf, sb_st, sb_en = sample
-    d_sb = torch.zeros(((sb_buf.size + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
-    d_sb[: sb_buf.size].copy_(torch.from_numpy(sb_buf))
-    d_sbs = torch.from_numpy(sb_st.view(np.int64)).to(dev)
-    d_sbe = torch.from_numpy(sb_en.view(np.int64)).to(dev)
-    sb_n = int(sb_st.shape[0])
 
-    def single():
-        dec.decode_device(d_sb.data_ptr(), sb_buf.size, d_sbs.data_ptr(), d_sbe.data_ptr(), sb_n,
-                          stream=stream.cuda_stream)
+def _public(m: dict) -> dict:
+    return {k: v for k, v in m.items() if not k.startswith("_")}
 
-    for _ in range(3):
-        single()
-    sb_ms = []
-    for _ in range(10):
-        a0 = torch.cuda.Event(enable_timing=True)
-        a1 = torch.cuda.Event(enable_timing=True)
-        a0.record(stream)
-        single()
-        a1.record(stream)
-        torch.cuda.synchronize(dev)
-        sb_ms.append(a0.elapsed_time(a1))
-    sb_ms = float(np.median(sb_ms))
-    sb_bytes = int((sb_en - sb_st).sum())
 
-    # HBM bytes per launch of the dominant kernel from the committed PMC passes of this workload
-    # (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM); null if none
-    traffic, traffic_src = None, None
-    tf = REPO / "profiles" / f"traffic_{args.config}.json"
-    if tf.is_file():
-        t = json.loads(tf.read_text())
-        if (dominant in t.get("kernel", "") or dominant == t.get("stage")) and args.files is None:
-            traffic, traffic_src = int(t["traffic_bytes"]), f"profiles/{tf.name}"
+# ------------------------------------------------------------------------------------------------
+def run(args) -> None:
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    # TFRG_BENCH_BACKEND=gloo rehearses the multi-rank path on fewer GPUs than ranks (ranks share
+    # devices round-robin); the driver's runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("TFRG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    if dist:
+        import torch.distributed as tdist
 
-    ms_step = elapsed / args.steps * 1e3
-    gib_s_rank = framed_bytes / (ms_step / 1e3) / 2**30
-    tot_bytes, tot_n = framed_bytes, n
-    if dist:  # every rank decodes its own shard: the whole job is the sum over ranks
-        t = torch.tensor([framed_bytes, n], dtype=torch.float64, device=cdev)
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            tdist.init_process_group(backend)
+
+    from tfr_reader import hip
+
+    dev = torch.device("cuda", local)
+    # a dedicated stream: torch's default stream has handle 0, which the C-ABI reads as "use the
+    # context's own stream", and events recorded on it would not bracket the decode
+    stream = torch.cuda.Stream(dev)
+    dec = hip.HipDecoder(local)
+    ctx = Ctx(dev, stream, dec, dist, backend)
+
+    only = args.only
+    if only in (None, "c4", "c4c2"):
+        w = c4_workload("c1" if only in (None, "c4") else "c2", rank, world, args.files_per_gpu)
+    else:
+        w = single_workload(only)
+    head = measure(ctx, w, args.steps, args.warmup, args.profile_steps)
+    hbm_read = stream_read_gbs(ctx, head["_d_bytes"])
+    head["roofline"]["achievable_read_GBps"] = round(hbm_read, 1)
+    elapsed = head["_elapsed"]
+    tot_bytes, tot_n = w.framed_bytes, w.n
+    if dist:
+        cdev = dev if backend == "nccl" else torch.device("cpu")
+        t = torch.tensor([w.framed_bytes, w.n], dtype=torch.float64, device=cdev)
         tdist.all_reduce(t, op=tdist.ReduceOp.SUM)
         tot_bytes, tot_n = float(t[0].item()), float(t[1].item())
     value = tot_bytes / (elapsed / args.steps) / 2**30
     ex_s = tot_n / (elapsed / args.steps)
+    del head["_d_bytes"]
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(sample, args.cpu_seconds, args.config)
+        cpu = cpu_baseline(w, args.cpu_seconds)
+
+    configs = {}
+    if world == 1 and only is None and not args.no_extra:
+        for name in ("c1file", "c2", "c3", "c4c2"):
+            cw = c4_workload("c2", 0, 1, args.files_per_gpu) if name == "c4c2" else single_workload(name)
+            m = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps)
+            del m["_d_bytes"], m["_elapsed"]
+            if not args.no_cpu:
+                m["cpu_baseline"] = cpu_baseline(cw, args.cpu_seconds)
+            configs[name] = m
+            del cw
 
     if dist:
         tdist.barrier()
     if rank == 0:
         metric = json.loads((REPO / "BASELINE.json").read_text())["metric"]
+        cfg = {
+            "workload": w.desc,
+            "records_per_gpu": w.n,
+            "framed_bytes_per_gpu": w.framed_bytes,
+            "parallelism": f"file-sharded x{world} (LPT by bytes, no collective on the data path)",
+            "per_gpu_GiB_s": head["GiB_s"],
+        }
+        if hasattr(w, "files_total"):
+            cfg.update(files_total=w.files_total, files_per_gpu=w.files_mine,
+                       lpt_max_over_mean=round(w.lpt_max_over_mean, 4))
         line = {
             "metric": metric,
             "value": round(value, 3),
@@ -321,50 +457,48 @@ def main() -> None:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 4),
+            "ms_per_step": head["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
-            "config": {
-                "workload": CONFIGS[args.config][1].format(files=files) + ", spec CRC-32C, resident in HBM",
-                "records_per_gpu": n,
-                "framed_bytes_per_gpu": framed_bytes,
-                "parallelism": f"file-sharded x{world} (no collective on the data path)",
-                "per_gpu_GiB_s": round(gib_s_rank, 3),
-            },
-            "kernels_ms": {k: round(v, 4) for k, v in kern_ms.items()},
-            "roofline": {
-                "kernel": dominant,
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": PEAK_HBM_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / PEAK_HBM_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "algorithmic_bytes_per_launch": a_bytes,
-                "achievable_read_GBps": round(hbm_read_gbs, 1),
-            },
-            "single_batch": {
-                "records": sb_n,
-                "framed_bytes": sb_bytes,
-                "ms": round(sb_ms, 4),
-                "GiB_s": round(sb_bytes / (sb_ms / 1e3) / 2**30, 3),
-                "examples_per_s": round(sb_n / (sb_ms / 1e3), 1),
-            },
-            "pipeline": {
-                "alg_bytes_R_plus_W": R + W,
-                "achieved_GBps": round((R + W) / (ms_step / 1e3) / 1e9, 1),
-                "frac": round((R + W) / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
-            },
+            "config": cfg,
+            "kernels_ms": head["kernels_ms"],
+            "roofline": head["roofline"],
+            "pipeline": head["pipeline"],
             "cpu_baseline": cpu,
         }
+        if configs:
+            line["configs"] = configs
         print(json.dumps(line), flush=True)
     dec.close()
     if dist:
         tdist.destroy_process_group()
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned(rank: int, argv: list[str], world: int, port: int) -> None:
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    run(parse_args(argv))
+
+
+def main() -> None:
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launched without torchrun: one process per GPU, spawned before anything touches the GPU
+        import torch.multiprocessing as mp
+
+        mp.start_processes(_spawned, args=(sys.argv[1:], args.gpus, _free_port()), nprocs=args.gpus, join=True,
+                           start_method="spawn")
+        return
+    run(args)
 
 
 if __name__ == "__main__":

@@ -32,8 +32,20 @@ extern "C" {
 #define TFRG_FLAG_SPEC_VARINT 2u  /* protobuf-spec int64 varints instead of the reference's
                                      int-width shift (decoder.pyx:44)               */
 #define TFRG_FLAG_NO_CRC 4u       /* skip the CRC-32C verdicts                                   */
+#define TFRG_FLAG_STRICT_CRC 8u   /* a record whose length field or either masked CRC-32C does not
+                                     match fails with TFRG_ERR_CRC (no values) instead of only
+                                     clearing its verdict bits; overrides TFRG_FLAG_NO_CRC      */
+#define TFRG_FLAG_MATERIALIZE_BYTES 16u /* also gather every bytes_list element's payload into a
+                                     contiguous device byte column (tfrg_columns.bytes_data) with
+                                     u64 offsets (bytes_offsets); default: (offset, len) views  */
 
 int tfrg_abi_version(void);
+/* Per-record status (tfrg_status.h) -> the reference's exception: its Python type name ("Exception",
+ * "UnicodeDecodeError", "AttributeError", "OSError", ...) and message text, literal for the
+ * decoder.pyx:49-297 exceptions ("Unsupported wire type: <aux>" for TFRG_ERR_WIRE_TYPE). The
+ * message pointer is thread-local storage, valid until the next call on the thread. */
+const char* tfrg_status_exception(int status);
+const char* tfrg_status_message(int status, int64_t aux);
 /* message of the last runtime failure on this thread */
 const char* tfrg_last_error(void);
 
@@ -110,6 +122,7 @@ typedef struct tfrg_info {
   uint32_t scan_timeout;    /* must be 0                                          */
   uint64_t kind_totals[4];  /* values per kind: [1] bytes elements, [2] floats, [3] int64s */
   uint64_t nbytes;
+  uint64_t bytes_data_len;  /* TFRG_FLAG_MATERIALIZE_BYTES: bytes in the byte column, else 0   */
 } tfrg_info;
 
 /* Waits for the last decode and returns its summary. */
@@ -132,6 +145,10 @@ typedef struct tfrg_columns {
   uint32_t* bytes_off;
   uint32_t* bytes_len;
   uint32_t* miss;
+  /* TFRG_FLAG_MATERIALIZE_BYTES only: element e of the bytes values is
+   * bytes_data[bytes_offsets[e] .. bytes_offsets[e + 1]) (kind_totals[1] + 1 offsets) */
+  uint8_t* bytes_data;
+  uint64_t* bytes_offsets;
 } tfrg_columns;
 
 /* device pointers of the last result (valid until the next decode / destroy) */

@@ -17,6 +17,8 @@
  *   decoder.pyx:164  UnicodeDecodeError from bytes(key).decode('utf-8')  (aux = key off<<32 | len)
  *   example/feature.py:106  AttributeError: Example(features=None)  (no Features field)
  *   reader.py:48-49  OSError: empty read for the byte range
+ * Code 15 exists only under TFRG_FLAG_STRICT_CRC (a TFRecord-spec integrity check the reference
+ * does not have). tfrg_status_message / tfrg_status_exception (tfrg.h) give the text.
  * Codes 32..35 are shapes on which the reference has undefined behaviour (segfault, reads past
  * the bytes object, non-terminating parse). The build reports them instead.
  */
@@ -39,6 +41,9 @@ enum tfrg_status {
   TFRG_ERR_KEY_UTF8 = 12,
   TFRG_ERR_FEATURES_NONE = 13,
   TFRG_ERR_READ = 14,
+  TFRG_ERR_CRC = 15,            /* TFRG_FLAG_STRICT_CRC: length field / masked CRC-32C mismatch
+                                   (not a reference error: the reference never checks CRCs;
+                                   aux = the record's verdict bits)                            */
   /* reference undefined behaviour */
   TFRG_UB_EMPTY_FEATURE = 32,   /* decoder.pyx:177 fields[0] of an empty vector (segfault)   */
   TFRG_UB_SHORT_MAP_ENTRY = 33, /* decoder.pyx:163,165 fields[0]/[1] out of range (segfault) */

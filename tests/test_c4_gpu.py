@@ -1,0 +1,67 @@
+"""C4 on the device (BASELINE.json configs[4]): a TFRecord directory sharded per
+file. Every G-rank partition is decoded shard by shard (ranks 0..G-1 one after another on cuda:0,
+the same work the G processes of ``bench.py --gpus G`` do on their own GPUs); the union must equal
+the whole-directory decode and the oracle, record by record, in (tfrecord_filename,
+tfrecord_start) order (reader.py:158).
+"""
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tests import _golden as G
+from tests.test_gpu_parity import raw_entries
+from tfr_reader import hip, shard, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows(sb: shard.ShardBatch, r: hip.BatchResult):
+    out = []
+    for j, (name, s, e) in enumerate(sb.index_rows()):
+        ent = raw_entries(r, j) if r.status[j] == 0 else None
+        out.append((name, s, e, int(r.status[j]), int(r.verdict[j]), repr(G.canon_entries(ent) if ent else ent)))
+    return out
+
+
+@pytest.fixture(scope="module")
+def directory(tmp_path_factory):
+    d = tmp_path_factory.mktemp("c4")
+    paths = synth.write_c4_dir(d, 10, "c1", base=3000)  # C0/C1-shaped files, +-50 % record counts
+    for f in range(3):  # C2-shaped (flowers) files: records above lane_max, wavefront kernels
+        p = d / f"z-flowers-{f}.tfrecord"
+        synth.c4_file(f, "c2", base=6).tofile(p)
+        paths.append(str(p))
+    return sorted(paths)
+
+
+def test_shards_union_equals_whole_directory_and_oracle(directory):
+    dec = hip.HipDecoder(0)
+    try:
+        whole_sb = shard.read_shard(directory)
+        whole = _rows(whole_sb, dec.decode(whole_sb.buf, whole_sb.starts, whole_sb.ends))
+        for world in (1, 2, 3, 4):
+            union = []
+            for rank in range(world):
+                mine = shard.shard_paths(directory, rank, world)
+                sb = shard.read_shard(mine)
+                union += _rows(sb, dec.decode(sb.buf, sb.starts, sb.ends))
+            union.sort(key=lambda x: (x[0], x[1]))
+            assert union == whole, world
+    finally:
+        dec.close()
+    orc = O.Oracle()
+    raw = whole_sb.buf.tobytes()
+    assert len(whole) == len(whole_sb) > 10 * 1500
+    for j, (s, e) in enumerate(zip(whole_sb.starts.tolist(), whole_sb.ends.tolist())):
+        st, _, ent = orc.decode(raw[s + 12 : e - 4])
+        assert whole[j][3] == st == 0 and whole[j][4] == 7, j
+        assert whole[j][5] == repr(G.canon_entries(ent)), j
+
+
+def test_lpt_shards_balanced_by_bytes(directory):
+    sizes = np.array([shard.read_shard([p]).nbytes for p in directory])
+    for world in (2, 4):
+        loads = [shard.read_shard(shard.shard_paths(directory, r, world)).nbytes for r in range(world)]
+        assert sum(loads) == sizes.sum()
+        assert max(loads) - min(loads) <= sizes.max()

@@ -22,3 +22,22 @@ def test_library_exports_every_declared_symbol():
     for name in declared_symbols():
         assert hasattr(lib, name), name
     assert lib.tfrg_abi_version() == 1
+
+
+def test_status_messages_match_the_python_mirror():
+    """tfrg_status_exception / tfrg_status_message give C callers the reference's exception type and
+    text (decoder.pyx:49-297) without tfr_reader: identical to _status.exception_for."""
+    from tfr_reader import _status as S
+
+    lib = N.lib()
+    codes = [c for c in range(0, 70) if c in S.MESSAGES or c in S.UB_CODES or c in (
+        S.ERR_WIRE_TYPE, S.ERR_FEATURES_NONE, S.ERR_READ, S.ERR_CRC, S.ST_LIMIT)]
+    assert len(codes) >= 19
+    for code in codes:
+        for aux in (0, 3, 7):
+            e = S.exception_for(code, aux)
+            assert lib.tfrg_status_exception(code).decode() == type(e).__name__, code
+            assert lib.tfrg_status_message(code, aux).decode() == str(e), code
+    assert lib.tfrg_status_message(S.ERR_WIRE_TYPE, 4).decode() == "Unsupported wire type: 4"
+    assert lib.tfrg_status_exception(S.ERR_KEY_UTF8).decode() == "UnicodeDecodeError"
+    assert lib.tfrg_status_exception(0).decode() == ""

@@ -58,7 +58,7 @@ def payload_batch(payloads):
 
 
 @pytest.mark.parametrize("lane_max,wave_stage", [(1 << 20, 1 << 20), (0, 1 << 20), (0, 0)])
-def test_golden_cases_bit_exact(dec, lane_max, wave_stage):
+def test_golden_cases_bit_exact(dec, orc, lane_max, wave_stage):
     """Every reference case (valid, malformed, fuzzed) in one device batch; lane_max=0 forces the
     wavefront-per-record kernels (LDS-staged, or streaming with wave_stage=0), 1 MiB the
     lane-per-record kernels."""
@@ -75,7 +75,8 @@ def test_golden_cases_bit_exact(dec, lane_max, wave_stage):
     for i, c in enumerate(cases):
         st, aux = int(r.status[i]), int(r.aux[i])
         ent = raw_entries(r, i) if st == 0 else None
-        err = G.check_against_golden(c["ref"], st, aux, ent, payloads[i])
+        ost = orc.decode(payloads[i])[0] if st in S.UB_CODES else None
+        err = G.check_against_golden(c["ref"], st, aux, ent, payloads[i], c["name"], ost)
         if err:
             bad.append(f"{c['name']}: {err}")
     assert not bad, "\n".join(bad[:15])
@@ -130,7 +131,7 @@ def test_c1_shape_vs_oracle(dec, orc):
     r = dec.decode(buf, st, en)
     assert r.info.n_big == 0
     assert (r.verdict == 7).all()
-    bad = _compare_to_oracle(r, orc, buf, st, en, check_crc=False, idx=range(0, 65536, 7))
+    bad = _compare_to_oracle(r, orc, buf, st, en)  # every record: values, key order, CRC verdicts
     assert not bad, bad[:10]
     labels = r.i64[int(r.slot_base[r.slot_key.index("label")]) :][:65536]
     assert np.array_equal(labels, np.arange(65536) % 1000)

@@ -1,12 +1,20 @@
-"""N>1 path on CPU: world_size-2 gloo process group, per-file sharding with no data collective."""
+"""N>1 path on CPU: world_size-2 gloo process group over a TFRecord directory sharded per file.
+
+Each rank computes the same LPT partition without communicating, loads and indexes only its own
+files (native framing index) and decodes them; decoding here uses the test oracle, the parity
+checker (there is no GPU on this host: the device decode of the same shards is
+tests/test_c4_gpu.py). The gathered union must equal the whole-directory index and decode, in the
+reference's (tfrecord_filename, tfrecord_start) order (reader.py:158).
+"""
 
 import os
 import socket
 
+import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from tfr_reader import shard
+from tfr_reader import shard, synth
 
 
 def test_lpt_partition_balanced_and_complete():
@@ -21,10 +29,32 @@ def test_lpt_partition_balanced_and_complete():
         shard.lpt_partition(sizes, 0)
 
 
+def test_c4_directory_partition_balance():
+    """The bench's C4 directory (32 files per GPU, +-50 % record counts): LPT keeps every rank
+    within a few percent of the mean at 2/4/8 GPUs."""
+    for world in (2, 4, 8):
+        sizes = synth.c4_file_sizes(32 * world, "c1")
+        loads = [int(sizes[p].sum()) for p in map(np.array, shard.lpt_partition(sizes, world))]
+        assert max(loads) / (sum(loads) / world) < 1.03, (world, loads)
+
+
 def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def _decode_rows(sb: shard.ShardBatch):
+    """(file, start, end, status, values digest) per record of a shard (oracle = checker)."""
+    from oracle import oracle as O
+
+    orc = O.Oracle()
+    raw = sb.buf.tobytes()
+    rows = []
+    for (name, fs, fe), s, e in zip(sb.index_rows(), sb.starts.tolist(), sb.ends.tolist()):
+        st, _, ent = orc.decode(raw[s + 12 : e - 4])
+        rows.append((name, fs, fe, st, repr(ent)))
+    return rows
 
 
 def _worker(rank, world, port, paths, out):
@@ -33,26 +63,32 @@ def _worker(rank, world, port, paths, out):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     mine = shard.shard_paths(paths, rank, world)
+    rows = _decode_rows(shard.read_shard(mine))
     gathered = [None] * world
-    dist.all_gather_object(gathered, mine)
+    dist.all_gather_object(gathered, (mine, rows))
     t = shard.max_over_ranks(float(rank + 1))
     dist.barrier()
     out[rank] = (gathered, t)
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_sharding(tmp_path):
-    from tfr_reader import synth, writer
-
-    paths = []
-    for f in range(7):  # uneven file sizes
-        p = tmp_path / f"part-{f:03d}.tfrecord"
-        writer.write_tfrecord(p, synth.c1_payloads(50 * (f + 1)))
-        paths.append(str(p))
+def test_two_rank_gloo_sharded_directory(tmp_path):
+    paths = sorted(synth.write_c4_dir(tmp_path, 9, "c1", base=300))
     mgr = mp.Manager()
     out = mgr.dict()
     mp.start_processes(_worker, args=(2, _free_port(), paths, out), nprocs=2, join=True, start_method="spawn")
     (g0, t0), (g1, t1) = out[0], out[1]
-    assert g0 == g1  # every rank computes the same partition without exchanging data
-    assert sorted(g0[0] + g0[1]) == sorted(paths) and not set(g0[0]) & set(g0[1])
     assert t0 == t1 == 2.0  # max-over-ranks timing
+    (m0, r0), (m1, r1) = g0
+    assert g0 == g1
+    assert sorted(m0 + m1) == paths and not set(m0) & set(m1)  # every file on exactly one rank
+    union = sorted(r0 + r1, key=lambda r: (r[0], r[1]))
+    whole = _decode_rows(shard.read_shard(paths))
+    assert union == whole
+    assert all(r[3] == 0 for r in whole) and len(whole) > 9 * 150
+    # the same offsets the dataset indexer writes (indexer.py:143-167 order after reader.py:158's sort)
+    from tfr_reader import indexer
+
+    idx = indexer.create_index_for_directory(str(tmp_path))
+    want = sorted(zip(idx["tfrecord_filename"], idx["tfrecord_start"], idx["tfrecord_end"]))
+    assert [(r[0], r[1], r[2]) for r in whole] == want

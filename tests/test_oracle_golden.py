@@ -33,7 +33,7 @@ def test_oracle_matches_reference_cases(orc, chunk):
     for c in CASES[chunk::8]:
         payload = bytes.fromhex(c["payload"])
         st, aux, ent = orc.decode(payload, compat=True)
-        err = G.check_against_golden(c["ref"], st, aux, ent, payload)
+        err = G.check_against_golden(c["ref"], st, aux, ent, payload, c["name"], st)
         if err:
             bad.append(f"{c['name']}: {err}")
     assert not bad, "\n".join(bad[:20])

@@ -74,8 +74,12 @@ struct tfrg_ctx {
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
   DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum;
+  DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
+  bool materialized = false;
   // last batch
   uint32_t n = 0;
+  uint64_t cap_hint = 0;  // tfrg_decode_host: total bytes of the given ranges (>= nbytes when they overlap)
+  hipEvent_t order_ev = nullptr;  // orders a decode on a new stream after the previous one
   uint64_t nbytes = 0;
   uint64_t cap_i64 = 0, cap_f32 = 0, cap_b = 0;
   bool have_result = false;
@@ -138,8 +142,10 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
-                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum};
+                 &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
+                 &c->bdata, &c->boff64, &c->blb, &c->bbig};
   for (DBuf* b : all) b->release();
+  if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
     for (auto& e : c->ev) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
@@ -192,6 +198,10 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   if (!c) return TFRG_E_ARG;
   HIP_TRY(hipSetDevice(c->device));
   if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  // a failure below may leave buffers reallocated: no schema and no result until this succeeds
+  c->have_result = false;
+  c->n_keys = c->n_slots = 0;
+  c->ht_mask = 0;
   uint32_t hsz = 16;
   while (hsz < 2 * n_keys + 2) hsz <<= 1;
   std::vector<uint32_t> ht(hsz, 0), hash(n_keys ? n_keys : 1), off(n_keys + 1), kw(2ull * (n_keys ? n_keys : 1));
@@ -282,14 +292,27 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
     if (st) return st;
   }
   HIP_TRY(hipSetDevice(c->device));
+  c->have_result = false;  // set again once this decode is enqueued
   hipStream_t st = stream ? (hipStream_t)stream : c->own_stream;
+  if (flags & TFRG_FLAG_STRICT_CRC) flags &= ~TFRG_FLAG_NO_CRC;  // strict mode needs the verdicts
+  // a decode on another stream than the previous one must not overtake it (shared arena)
+  if (c->last_stream && c->last_stream != st) {
+    if (!c->order_ev) HIP_TRY(hipEventCreateWithFlags(&c->order_ev, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->order_ev, c->last_stream));
+    HIP_TRY(hipStreamWaitEvent(st, c->order_ev, 0));
+  }
   const uint32_t S = c->n_slots;
   const uint64_t nn = n ? n : 1;
   const uint32_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
   const uint32_t tile_stride = (n_tiles + 3u) & ~3u;
   const uint32_t n_chunks = (n_tiles + (1u << kSpineChunkShift) - 1u) >> kSpineChunkShift;
   const uint64_t tsum_words = (uint64_t)S * tile_stride + 2ull * S * n_chunks;  // tile sums + look-back words
-  const uint64_t cap_i64 = nbytes + 16, cap_f32 = nbytes / 4 + 16, cap_b = nbytes / 2 + 16;
+  // value capacities: bounds for disjoint ranges (one int64 per byte, one float per 4, one bytes
+  // element per 2); tfrg_decode_host passes the total of its ranges, which covers overlaps. A batch
+  // of overlapping device ranges that exceeds them is reported by tfrg_result_info (TFRG_E_LIMIT).
+  const uint64_t cap_in = c->cap_hint > nbytes ? c->cap_hint : nbytes;
+  c->cap_hint = 0;
+  const uint64_t cap_i64 = cap_in + 16, cap_f32 = cap_in / 4 + 16, cap_b = cap_in / 2 + 16;
   // growing an arena buffer frees the old one: wait for work that may still read it
   bool grow = c->status.cap < nn * 4 || c->aux.cap < nn * 8 || c->verdict.cap < nn ||
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
@@ -312,6 +335,20 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
   if (S && n) HIP_TRY(hipMemsetAsync(c->tsum.p, 0, tsum_words * 4, st));
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
+  const bool mat = (flags & TFRG_FLAG_MATERIALIZE_BYTES) != 0;
+  const uint64_t lb_words = materialize_lb_words(cap_b);
+  if (mat) {
+    const bool g2 = c->bdata.cap < cap_in + 16 || c->boff64.cap < (cap_b + 1) * 8 || c->blb.cap < lb_words * 8 ||
+                    c->bbig.cap < cap_b * 4;
+    if (g2 && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    if (c->bdata.ensure(cap_in + 16) || c->boff64.ensure((cap_b + 1) * 8) || c->blb.ensure(lb_words * 8) ||
+        c->bbig.ensure(cap_b * 4)) {
+      set_error("device allocation failed (materialized bytes)");
+      return TFRG_E_NOMEM;
+    }
+    HIP_TRY(hipMemsetAsync(c->blb.p, 0, lb_words * 8, st));
+    if (!n) HIP_TRY(hipMemsetAsync(c->boff64.p, 0, 8, st));
+  }
   if (!S || !n) HIP_TRY(hipMemsetAsync(c->kind_totals.p, 0, 32, st));
 
   DevBatch b;
@@ -368,6 +405,27 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       ev = c->ev;
     }
     hipError_t e = launch_decode(b, schema_view(c), o, cfg, c->crc_tab.as<uint32_t>(), c->consts.as<uint32_t>(), st, ev);
+    if (e == hipSuccess && mat && S) {
+      DevBytes d;
+      d.in = d_bytes;
+      d.in_readable = (nbytes + 15) & ~15ull;
+      d.b_off = o.b_off;
+      d.b_len = o.b_len;
+      d.kind_totals = o.kind_totals;
+      d.offsets = c->boff64.as<uint64_t>();
+      d.offsets_cap = cap_b;
+      d.data = c->bdata.as<uint8_t>();
+      d.data_cap = cap_in + 16;
+      d.lb = c->blb.as<uint64_t>();
+      d.ticket = o.info + kInfoBytesTicket;
+      d.big_count = o.info + kInfoBytesBig;
+      d.big_list = c->bbig.as<uint32_t>();
+      d.overflow = o.info + kInfoOverflow;
+      e = launch_materialize(d, c->num_cus, st);
+    } else if (e == hipSuccess && mat) {
+      e = hipMemsetAsync(c->boff64.p, 0, 8, st);  // no slots: no elements
+    }
+    if (ev && e == hipSuccess) e = hipEventRecord(ev[kNumStages], st);
     if (e != hipSuccess) {
       set_error(std::string("kernel launch: ") + hipGetErrorString(e));
       return TFRG_E_HIP;
@@ -379,6 +437,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   c->cap_f32 = cap_f32;
   c->cap_b = cap_b;
   c->last_stream = st;
+  c->materialized = mat;
   c->have_result = true;
   return 0;
 }
@@ -401,6 +460,12 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
     HIP_TRY(hipMemcpyAsync(c->in_start.p, h_start, (size_t)n * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(c->in_end.p, h_end, (size_t)n * 8, hipMemcpyHostToDevice, st));
   }
+  uint64_t total = 0;  // bytes of all ranges (clamped to the buffer): repeated ranges count again
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint64_t a = h_start[i], b = h_end[i] < nbytes ? h_end[i] : nbytes;
+    if (b > a) total += b - a;
+  }
+  c->cap_hint = total;
   return tfrg_decode_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_start.as<uint64_t>(),
                             c->in_end.as<uint64_t>(), n, flags, st);
 }
@@ -413,6 +478,11 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   HIP_TRY(hipMemcpyAsync(h, c->info.p, sizeof(h), hipMemcpyDeviceToHost, c->last_stream));
   HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
   HIP_TRY(hipStreamSynchronize(c->last_stream));
+  uint64_t blen = 0;
+  if (c->materialized && !h[kInfoOverflow]) {  // the byte column's length: offsets[nb]
+    const uint64_t nb = c->n ? kt[TFRG_KIND_BYTES] : 0;
+    HIP_TRY(hipMemcpy(&blen, c->boff64.as<uint64_t>() + nb, 8, hipMemcpyDeviceToHost));
+  }
   memset(info, 0, sizeof(*info));
   info->n_records = c->n;
   info->n_slots = c->n_slots;
@@ -424,6 +494,12 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->scan_timeout = h[kInfoScanTimeout];
   for (int k = 0; k < 4; ++k) info->kind_totals[k] = kt[k];
   info->nbytes = c->nbytes;
+  info->bytes_data_len = blen;
+  if (h[kInfoOverflow]) {
+    set_error("value columns overflowed their capacity (overlapping ranges in a device batch): decode "
+              "the ranges from host memory (tfrg_decode_host) or split the batch");
+    return TFRG_E_LIMIT;
+  }
   return 0;
 }
 
@@ -440,6 +516,8 @@ int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
   d->bytes_off = c->b_off.as<uint32_t>();
   d->bytes_len = c->b_len.as<uint32_t>();
   d->miss = c->miss.as<uint32_t>();
+  d->bytes_data = c->materialized ? c->bdata.as<uint8_t>() : nullptr;
+  d->bytes_offsets = c->materialized ? c->boff64.as<uint64_t>() : nullptr;
   return 0;
 }
 
@@ -459,10 +537,16 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
   HIP_TRY(cp(h->order, c->order.p, S * n * 2));
   HIP_TRY(cp(h->row_splits, c->rs.p, S * (n + 1) * 4));
   HIP_TRY(cp(h->slot_base, c->slot_base.p, S * 8));
-  HIP_TRY(cp(h->i64, c->i64.p, info.kind_totals[TFRG_KIND_INT64] * 8));
-  HIP_TRY(cp(h->f32, c->f32.p, info.kind_totals[TFRG_KIND_FLOAT] * 4));
-  HIP_TRY(cp(h->bytes_off, c->b_off.p, info.kind_totals[TFRG_KIND_BYTES] * 4));
-  HIP_TRY(cp(h->bytes_len, c->b_len.p, info.kind_totals[TFRG_KIND_BYTES] * 4));
+  // (clamped to the capacities: a result that overflowed them fails in tfrg_result_info above)
+  auto cl = [](uint64_t v, uint64_t cap) { return v < cap ? v : cap; };
+  HIP_TRY(cp(h->i64, c->i64.p, cl(info.kind_totals[TFRG_KIND_INT64], c->cap_i64) * 8));
+  HIP_TRY(cp(h->f32, c->f32.p, cl(info.kind_totals[TFRG_KIND_FLOAT], c->cap_f32) * 4));
+  HIP_TRY(cp(h->bytes_off, c->b_off.p, cl(info.kind_totals[TFRG_KIND_BYTES], c->cap_b) * 4));
+  HIP_TRY(cp(h->bytes_len, c->b_len.p, cl(info.kind_totals[TFRG_KIND_BYTES], c->cap_b) * 4));
+  if (c->materialized) {
+    HIP_TRY(cp(h->bytes_data, c->bdata.p, info.bytes_data_len));
+    HIP_TRY(cp(h->bytes_offsets, c->boff64.p, (info.kind_totals[TFRG_KIND_BYTES] + 1) * 8));
+  }
   const size_t nm = info.n_miss_entries < kMissCap ? info.n_miss_entries : kMissCap;
   HIP_TRY(cp(h->miss, c->miss.p, nm * 16));
   HIP_TRY(hipStreamSynchronize(st));

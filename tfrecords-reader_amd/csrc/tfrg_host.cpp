@@ -66,6 +66,75 @@ int tfrg_abi_version(void) { return TFRG_ABI_VERSION; }
 const char* tfrg_last_error(void) { return g_last_error.c_str(); }
 void tfrg_free(void* p) { free(p); }
 
+// Per-record status -> the exception the reference raises (decoder.pyx:49-297, feature.py:106,
+// reader.py:48-49), for C / Cython callers that do not go through tfr_reader/_status.py.
+const char* tfrg_status_exception(int status) {
+  switch (status) {
+    case TFRG_OK: return "";
+    case TFRG_ERR_KEY_UTF8: return "UnicodeDecodeError";  // bytes(key).decode('utf-8'), decoder.pyx:164
+    case TFRG_ERR_FEATURES_NONE: return "AttributeError";  // Example(features=None).feature, feature.py:106
+    case TFRG_ERR_READ: return "OSError";                 // reader.py:48-49
+    case TFRG_ERR_CRC: return "DataLossError";             // TFRG_FLAG_STRICT_CRC (OSError subclass)
+    case TFRG_UB_EMPTY_FEATURE: case TFRG_UB_SHORT_MAP_ENTRY: case TFRG_UB_NEGATIVE_LENGTH:
+    case TFRG_UB_READ_PAST_END: return "UndefinedRecordError";
+    case TFRG_ST_SCHEMA_MISS: case TFRG_ST_LIMIT: return "RuntimeError";
+    default: return status >= TFRG_ERR_VARINT_TOO_MANY && status <= TFRG_ERR_WT_INT64_LIST ? "Exception"
+                                                                                             : "RuntimeError";
+  }
+}
+
+const char* tfrg_status_message(int status, int64_t aux) {
+  static thread_local char buf[256];
+  const char* m = nullptr;
+  switch (status) {
+    case TFRG_OK: m = ""; break;
+    case TFRG_ERR_VARINT_TOO_MANY: m = "Too many bytes when decoding varint."; break;                   // :49
+    case TFRG_ERR_EOB_FIXED64: m = "Unexpected end of buffer when reading fixed64."; break;              // :79
+    case TFRG_ERR_EOB_LEN: m = "Unexpected end of buffer when reading length-delimited field."; break;  // :89
+    case TFRG_ERR_EOB_FIXED32: m = "Unexpected end of buffer when reading fixed32."; break;              // :98
+    case TFRG_ERR_WIRE_TYPE:                                                                            // :104
+      snprintf(buf, sizeof(buf), "Unsupported wire type: %lld", (long long)aux);
+      return buf;
+    case TFRG_ERR_WT_FEATURES: m = "Unexpected wire type for field features"; break;  // :123
+    case TFRG_ERR_WT_FEATURE: m = "Unexpected wire type for field feature"; break;    // :147
+    case TFRG_ERR_FEATURE_FIELD: m = "Unexpected field number in Feature"; break;     // :199
+    case TFRG_ERR_WT_BYTES_LIST: m = "Unexpected wire type in BytesList"; break;      // :220
+    case TFRG_ERR_WT_FLOAT_LIST: m = "Unexpected wire type in FloatList"; break;      // :264
+    case TFRG_ERR_WT_INT64_LIST: m = "Unexpected wire type in Int64List"; break;      // :297
+    case TFRG_ERR_KEY_UTF8:
+      snprintf(buf, sizeof(buf), "'utf-8' codec can't decode the key at payload offset %llu (length %llu)",
+               (unsigned long long)((uint64_t)aux >> 32), (unsigned long long)((uint64_t)aux & 0xffffffffu));
+      return buf;
+    case TFRG_ERR_FEATURES_NONE: m = "'NoneType' object has no attribute 'feature'"; break;
+    case TFRG_ERR_READ: m = "Failed to read data for the record byte range!"; break;
+    case TFRG_ERR_CRC:
+      snprintf(buf, sizeof(buf),
+               "corrupted record: length field / masked CRC-32C mismatch (verdict bits 0x%llx)",
+               (unsigned long long)aux);
+      return buf;
+    case TFRG_UB_EMPTY_FEATURE:
+      m = "Feature has no kind field (the reference reads fields[0] of an empty vector and crashes: "
+          "decoder.pyx:177)";
+      break;
+    case TFRG_UB_SHORT_MAP_ENTRY:
+      m = "map entry has fewer than two fields (the reference reads fields[1] out of range and crashes: "
+          "decoder.pyx:163-165)";
+      break;
+    case TFRG_UB_NEGATIVE_LENGTH:
+      m = "negative length-delimited size (undefined in the reference: decoder.pyx:85-92 moves the cursor "
+          "backwards)";
+      break;
+    case TFRG_UB_READ_PAST_END:
+      m = "varint runs past the end of the record (undefined in the reference: decoder.pyx:34-50 has no bound)";
+      break;
+    case TFRG_ST_LIMIT: m = "record exceeds a decoder limit (more than 65534 keys)"; break;
+    default:
+      snprintf(buf, sizeof(buf), "unexpected decoder status %d", status);
+      return buf;
+  }
+  return m;
+}
+
 uint32_t tfrg_crc32c(const uint8_t* p, uint64_t n) { return ~host_crc().update(0xffffffffu, p, n); }
 uint32_t tfrg_masked_crc32c(const uint8_t* p, uint64_t n) { return crc_mask(tfrg_crc32c(p, n)); }
 

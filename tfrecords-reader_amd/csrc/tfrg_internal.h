@@ -71,6 +71,9 @@ enum InfoIdx : uint32_t {
   kInfoSpineDone = 8,    // spine workgroups finished (the last one computes the column bases)
   kInfoNeed = 9,         // lane records with an out-of-line list (k_list_gather; listed in slow_list)
   kInfoSpineTicket = 10, // k_spine workgroup tickets (chunk order of the look-back)
+  kInfoOverflow = 11,    // a kind's value total exceeds its column capacity (overlapping ranges)
+  kInfoBytesTicket = 12, // k_bytes_scan tile tickets
+  kInfoBytesBig = 13,    // k_bytes_scan: long elements listed for the wave copy
   kInfoCount = 16
 };
 
@@ -116,7 +119,29 @@ constexpr uint32_t kSpineChunkShift = 12;
 constexpr uint32_t kFlagPayloadOnly = 1u;
 constexpr uint32_t kFlagSpecVarint = 2u;
 constexpr uint32_t kFlagNoCrc = 4u;
+constexpr uint32_t kFlagStrictCrc = 8u;
+constexpr uint32_t kFlagMaterializeBytes = 16u;
 
+
+// TFRG_FLAG_MATERIALIZE_BYTES (tfrg_bytes.hip): bytes_list elements gathered into one column
+struct DevBytes {
+  const uint8_t* in;             // batch bytes
+  uint64_t in_readable;          // round_up(nbytes, 16)
+  const uint32_t* b_off;         // element views (absolute offset, length)
+  const uint32_t* b_len;
+  const uint64_t* kind_totals;   // [1] = element count (k_spine)
+  uint64_t* offsets;             // [nb + 1] exclusive prefix of the lengths
+  uint64_t offsets_cap;          // elements the offsets buffer holds (cap_b)
+  uint8_t* data;                 // the byte column
+  uint64_t data_cap;
+  uint64_t* lb;                  // look-back words (zeroed per decode)
+  uint32_t* ticket;              // scan tile tickets (zeroed per decode)
+  uint32_t* big_count;           // elements longer than the short-copy bound (zeroed per decode)
+  uint32_t* big_list;            // [cap_b]
+  uint32_t* overflow;            // info[kInfoOverflow]
+};
+hipError_t launch_materialize(const DevBytes& d, int num_cus, hipStream_t st);
+uint64_t materialize_lb_words(uint64_t cap_b);
 
 // launchers (tfrg_kernels.hip)
 struct LaunchCfg {
@@ -129,7 +154,7 @@ struct LaunchCfg {
 
 // Kernel stages, in launch order (profiling events bracket each one).
 enum Stage : int { kStageLaneCount = 0, kStageSlowCount, kStageWaveCount, kStageSpine, kStageDownGather,
-                   kStageListGather, kStageWaveGather, kNumStages };
+                   kStageListGather, kStageWaveGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

@@ -680,6 +680,14 @@ __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int s
   }
 }
 
+// TFRG_FLAG_STRICT_CRC: a framed record is accepted only with a matching length field and masked
+// CRC-32Cs (need_data = false while the payload CRC is still k_big_crc's work).
+__device__ __forceinline__ bool strict_pass(const DevBatch& B, uint32_t verdict, bool need_data) {
+  if (!(B.flags & kFlagStrictCrc) || (B.flags & kFlagPayloadOnly)) return true;
+  const uint32_t need = TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | (need_data ? TFRG_V_DATA_CRC : 0u);
+  return (verdict & need) == need;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Wave staging for the lane-per-record kernels: the 64 records of a wave are (in the common case of
 // whole-file batches) one contiguous span of a few KiB. The wave copies that span into its LDS stage
@@ -1449,9 +1457,11 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       PHASE_MARK(p2);
       PHASE_ADD(17, p1, p2);
       sink.fast_reset(S);
-      const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-      done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
-      tried = true;
+      if (strict_pass(B, v.verdict, true)) {  // (strict mode: a CRC failure is the slow kernel's)
+        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+        done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+        tried = true;
+      }
       PHASE_MARK(p3);
       PHASE_ADD(18, p2, p3);
     }
@@ -1464,9 +1474,11 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       if (bigw) {
         frame_verdicts<R, false>(B, v, T, nullptr, 0, mine);
         sink.fast_reset(S);
-        const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
-        done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
-        tried = true;
+        if (strict_pass(B, v.verdict, mine)) {
+          const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
+          done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+          tried = true;
+        }
       }
     }
     PHASE_MARK(p4);
@@ -1551,6 +1563,10 @@ __global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema
       s.init(B.bytes, v.p0, v.L);
       status = walk_example<COMPAT>(s, sink, aux);
       if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
+      if (status == TFRG_OK && !strict_pass(B, v.verdict, v.e - v.st <= lane_max)) {
+        status = TFRG_ERR_CRC;  // (records above lane_max: their payload CRC is k_big_crc's)
+        aux = v.verdict;
+      }
     }
     sink.finalize(status == TFRG_OK);
     record_result(o, r, status, aux, v.verdict);
@@ -1703,8 +1719,36 @@ __device__ __forceinline__ uint32_t crc_one_wave(const uint8_t* buf, uint64_t a,
 // Payload CRC-32C of every record above lane_max (their framing bits and walk are the lane / slow
 // kernels'), the DATA_CRC verdict bit OR-ed into the verdict column. Records whose span fits the
 // wave stage (the front of big_list) take one WAVE each; larger ones one WORKGROUP each.
+// TFRG_FLAG_STRICT_CRC, payload CRC of a record above lane_max failed: the record becomes an error
+// (status TFRG_ERR_CRC, aux = verdict) and its counts are withdrawn from the columns and the tile
+// sums before k_spine scans them. `t` indexes the slots with stride `nt` (the calling wave / group).
+__device__ void strict_reject(const DevOut& o, uint32_t n, uint32_t n_slots, uint32_t r, uint32_t verdict,
+                              uint32_t t, uint32_t nt) {
+  if (__hip_atomic_load(&o.status[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != TFRG_OK) return;
+  for (uint32_t k = t; k < n_slots; k += nt) {
+    const size_t at = (size_t)k * n + r;
+    const uint32_t c = o.count[at];
+    if (o.order[at]) o.order[at] = 0;  // (present slots with empty lists have count 0)
+    if (!c) continue;
+    o.count[at] = 0;
+    if (c & ~kCountInline) atomicSub(&o.tsum[(size_t)k * o.tile_stride + (r >> kTileShift)], c & ~kCountInline);
+  }
+  if (t == 0) {
+    o.status[r] = TFRG_ERR_CRC;
+    o.aux[r] = verdict;
+    atomicAdd(&o.info[kInfoErrors], 1u);
+    atomicMin(&o.info[kInfoFirstError], r);
+  }
+}
+
+// a matching payload CRC; a strict-mode rejection of the slow kernel (length CRC) keeps aux = verdict
+__device__ __forceinline__ void set_data_crc(const DevBatch& B, const DevOut& o, uint32_t r) {
+  o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
+  if ((B.flags & kFlagStrictCrc) && o.status[r] == TFRG_ERR_CRC) o.aux[r] |= TFRG_V_DATA_CRC;
+}
+
 __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, const uint32_t* __restrict__ crc_tab,
-                                                       const uint32_t* __restrict__ consts) {
+                                                       const uint32_t* __restrict__ consts, uint32_t n_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;           // [4][256] slice-by-4
   uint32_t* A1 = lds + 1024;     // [4][256] (x) x^8192
@@ -1727,7 +1771,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     if (v.e - v.st < 16) continue;
     const uint64_t a = v.p0, b = v.e - 4;
     const uint32_t c = b - a >= 64 ? crc_one_wave(B.bytes, a, b, T, A1, cst, lane) : crc_serial<1>(B.bytes, a, b, T);
-    if (lane == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
+    const bool good = crc_mask(c) == load_u32_unaligned(B.bytes, b);
+    if (lane == 0 && good) set_data_crc(B, o, r);
+    if (!good && (B.flags & kFlagStrictCrc)) strict_reject(o, B.n, n_slots, r, o.verdict[r], lane, 64);
   }
   // larger records: one workgroup each
   for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {  // workgroup-uniform
@@ -1749,7 +1795,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     } else {
       c = crc_serial<1>(B.bytes, a, b, T);
     }
-    if (threadIdx.x == 0 && crc_mask(c) == load_u32_unaligned(B.bytes, b)) o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
+    const bool good = crc_mask(c) == load_u32_unaligned(B.bytes, b);
+    if (threadIdx.x == 0 && good) set_data_crc(B, o, r);
+    if (!good && (B.flags & kFlagStrictCrc) && threadIdx.x < 64)
+      strict_reject(o, B.n, n_slots, r, o.verdict[r], threadIdx.x, 64);
     PHASE_MARK(h1);
     if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
   }
@@ -1923,8 +1972,13 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
     }
     __syncthreads();
   }
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+    // capacities bound the values of disjoint ranges; overlapping / repeated ranges can exceed
+    // them (stores past a capacity are dropped): the host reports TFRG_E_LIMIT
+    if (acc[TFRG_KIND_INT64] > o.cap_i64 || acc[TFRG_KIND_FLOAT] > o.cap_f32 || acc[TFRG_KIND_BYTES] > o.cap_b)
+      o.info[kInfoOverflow] = 1u;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2472,7 +2526,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
 const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_slow_count",  "k_big_crc",    "k_spine",
-                                             "k_down_gather", "k_list_gather", "k_wave_gather"};
+                                             "k_down_gather", "k_list_gather", "k_wave_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -2532,7 +2586,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   mark(kStageWaveCount);
   {
     const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
-    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (3072 + 128 + 4) * 4, st, b, o, d_tab, d_consts);
+    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (3072 + 128 + 4) * 4, st, b, o, d_tab, d_consts,
+                       (uint32_t)S);
   }
   mark(kStageSpine);
   if (S > 0)
@@ -2561,7 +2616,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, sc, o);
     hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
   }
-  mark(kNumStages);
+  mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)
   return hipGetLastError();
 }
 

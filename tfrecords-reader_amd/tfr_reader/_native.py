@@ -33,6 +33,7 @@ class TfrgInfo(C.Structure):
         ("scan_timeout", C.c_uint32),
         ("kind_totals", C.c_uint64 * 4),
         ("nbytes", C.c_uint64),
+        ("bytes_data_len", C.c_uint64),
     ]
 
 
@@ -49,6 +50,8 @@ class TfrgColumns(C.Structure):
         ("bytes_off", u32p),
         ("bytes_len", u32p),
         ("miss", u32p),
+        ("bytes_data", u8p),
+        ("bytes_offsets", u64p),
     ]
 
 
@@ -56,6 +59,8 @@ class TfrgColumns(C.Structure):
 SIGNATURES: dict[str, tuple] = {
     "tfrg_abi_version": (C.c_int, []),
     "tfrg_last_error": (C.c_char_p, []),
+    "tfrg_status_exception": (C.c_char_p, [C.c_int]),
+    "tfrg_status_message": (C.c_char_p, [C.c_int, C.c_int64]),
     "tfrg_index_buffer": (C.c_int64, [C.c_void_p, C.c_uint64, u64p, C.c_int64]),
     "tfrg_index_file": (C.c_int, [C.c_char_p, C.POINTER(u64p), i64p]),
     "tfrg_idx_save": (C.c_int, [C.c_char_p, u64p, C.c_int64]),
@@ -91,6 +96,8 @@ SIGNATURES: dict[str, tuple] = {
 FLAG_PAYLOAD_ONLY = 1
 FLAG_SPEC_VARINT = 2
 FLAG_NO_CRC = 4
+FLAG_STRICT_CRC = 8
+FLAG_MATERIALIZE_BYTES = 16
 
 
 class NativeError(RuntimeError):

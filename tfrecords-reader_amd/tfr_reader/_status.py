@@ -23,6 +23,7 @@ ERR_WT_INT64_LIST = 11
 ERR_KEY_UTF8 = 12
 ERR_FEATURES_NONE = 13
 ERR_READ = 14
+ERR_CRC = 15
 UB_EMPTY_FEATURE = 32
 UB_SHORT_MAP_ENTRY = 33
 UB_NEGATIVE_LENGTH = 34
@@ -61,6 +62,11 @@ class UndefinedRecordError(Exception):
     """A record shape on which the reference has undefined behaviour (crash / garbage)."""
 
 
+class DataLossError(OSError):
+    """TFRG_FLAG_STRICT_CRC: a framed record whose length field or masked CRC-32C does not match
+    (the TFRecord spec's integrity check; the reference never verifies CRCs)."""
+
+
 def exception_for(status: int, aux: int, payload_key: bytes | None = None) -> BaseException:
     """Build the exception the reference raises for this per-record status.
 
@@ -81,6 +87,8 @@ def exception_for(status: int, aux: int, payload_key: bytes | None = None) -> Ba
         return AttributeError("'NoneType' object has no attribute 'feature'")
     if status == ERR_READ:
         return OSError("Failed to read data for the record byte range!")
+    if status == ERR_CRC:
+        return DataLossError(f"corrupted record: length field / masked CRC-32C mismatch (verdict bits {aux:#x})")
     if status in UB_CODES:
         return UndefinedRecordError(UB_MESSAGES[status])
     if status == ST_LIMIT:

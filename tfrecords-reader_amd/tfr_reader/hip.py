@@ -71,8 +71,6 @@ class KeyTable:
 class HipDecoder:
     """One device context (one HIP device, one host thread at a time)."""
 
-    MAX_SCHEMA_ROUNDS = 64
-
     def __init__(self, device: int = 0, spec_varint: bool = False, keys: KeyTable | None = None) -> None:
         self._lib = N.lib()
         self.device = device
@@ -137,7 +135,7 @@ class HipDecoder:
         self._pushed = kt.version
 
     # ------------------------------------------------------------------ decode
-    def _flags(self, payload_only: bool, crc: bool) -> int:
+    def _flags(self, payload_only: bool, crc: bool, strict_crc: bool = False, materialize_bytes: bool = False) -> int:
         f = 0
         if payload_only:
             f |= N.FLAG_PAYLOAD_ONLY
@@ -145,6 +143,10 @@ class HipDecoder:
             f |= N.FLAG_SPEC_VARINT
         if not crc:
             f |= N.FLAG_NO_CRC
+        if strict_crc:
+            f |= N.FLAG_STRICT_CRC
+        if materialize_bytes:
+            f |= N.FLAG_MATERIALIZE_BYTES
         return f
 
     def info(self) -> N.TfrgInfo:
@@ -176,17 +178,27 @@ class HipDecoder:
         *,
         payload_only: bool = False,
         crc: bool = True,
+        strict_crc: bool = False,
+        materialize_bytes: bool = False,
     ) -> BatchResult:
-        """Decode records [starts[i], ends[i]) of a host buffer (framed unless payload_only)."""
+        """Decode records [starts[i], ends[i]) of a host buffer (framed unless payload_only).
+
+        ``strict_crc``: records whose length field or masked CRC-32C does not match fail with
+        ``DataLossError`` (TFRG_FLAG_STRICT_CRC) instead of only clearing their verdict bits.
+        ``materialize_bytes``: bytes_list payloads are gathered on the device into one byte column
+        (``BatchResult.bytes_data`` / ``bytes_offsets``) and fetched, instead of being sliced from
+        the host copy of the input."""
         buf = _as_u8(buf)
         st = np.ascontiguousarray(starts, dtype=np.uint64)
         en = np.ascontiguousarray(ends, dtype=np.uint64)
         if st.shape != en.shape:
             raise ValueError("starts and ends differ in length")
         n = int(st.shape[0])
-        flags = self._flags(payload_only, crc)
+        flags = self._flags(payload_only, crc, strict_crc, materialize_bytes)
         with self._lock:
-            for _ in range(self.MAX_SCHEMA_ROUNDS):
+            # every round interns at least one new key (else it raises), and at most 65,536 miss
+            # entries are reported per round, so high-cardinality key sets take several rounds
+            while True:
                 self.push_schema()
                 N.check(
                     self._lib.tfrg_decode_host(
@@ -202,23 +214,22 @@ class HipDecoder:
                     break
                 if not self._learn_misses(buf, info):
                     raise N.NativeError("schema misses reported but no new key learned")
-            else:
-                raise N.NativeError("schema did not converge")
-            return self._fetch(buf, st, en, info, payload_only)
+            return self._fetch(buf, st, en, info, payload_only, materialize_bytes)
 
     def decode_device(self, d_bytes: int, nbytes: int, d_start: int, d_end: int, n: int, *,
-                      payload_only: bool = False, crc: bool = True, stream: int | None = None) -> None:
+                      payload_only: bool = False, crc: bool = True, stream: int | None = None,
+                      strict_crc: bool = False, materialize_bytes: bool = False) -> None:
         """Asynchronous decode of a device-resident batch (raw device pointers; bench path)."""
         self.push_schema()
         N.check(
             self._lib.tfrg_decode_device(
                 self._ctx, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_start), C.c_void_p(d_end), n,
-                self._flags(payload_only, crc), C.c_void_p(stream) if stream else None,
+                self._flags(payload_only, crc, strict_crc, materialize_bytes), C.c_void_p(stream) if stream else None,
             ),
             "tfrg_decode_device",
         )
 
-    def _fetch(self, buf, st, en, info: N.TfrgInfo, payload_only: bool) -> BatchResult:
+    def _fetch(self, buf, st, en, info: N.TfrgInfo, payload_only: bool, materialize: bool = False) -> BatchResult:
         n, ns = info.n_records, info.n_slots
         kt = info.kind_totals
         r = BatchResult()
@@ -233,9 +244,14 @@ class HipDecoder:
         r.f32 = np.empty(kt[2], np.uint32)
         r.bytes_off = np.empty(kt[1], np.uint32)
         r.bytes_len = np.empty(kt[1], np.uint32)
+        names = ["status", "aux", "verdict", "order", "row_splits", "slot_base", "i64", "f32", "bytes_off",
+                 "bytes_len"]
+        if materialize:
+            r.bytes_data = np.empty(info.bytes_data_len, np.uint8)
+            r.bytes_offsets = np.empty(kt[1] + 1, np.uint64)
+            names += ["bytes_data", "bytes_offsets"]
         cols = N.TfrgColumns()
-        for name in ("status", "aux", "verdict", "order", "row_splits", "slot_base", "i64", "f32",
-                     "bytes_off", "bytes_len"):
+        for name in names:
             arr = getattr(r, name)
             setattr(cols, name, N.ptr(arr, dict(N.TfrgColumns._fields_)[name]))
         N.check(self._lib.tfrg_result_fetch(self._ctx, C.byref(cols)), "tfrg_result_fetch")
@@ -264,7 +280,19 @@ class BatchResult:
     bytes_len: np.ndarray
     slot_key: list[str]
     slot_kind: list[int]
+    bytes_data: np.ndarray | None = None  # materialize_bytes: the device-gathered byte column
+    bytes_offsets: np.ndarray | None = None  # its u64 offsets (one per bytes element, + 1)
     _lay = None  # (record -> layout index, layouts), built on first use
+
+    def _bytes_elems(self, lo: int, hi: int) -> list[bytes]:
+        """bytes elements [lo, hi) of the bytes value array, as ``bytes``."""
+        if self.bytes_data is not None:
+            o = self.bytes_offsets[lo : hi + 1].tolist()
+            d = self.bytes_data
+            return [d[o[j] : o[j + 1]].tobytes() for j in range(hi - lo)]
+        b = self.buf
+        return [b[o : o + ln].tobytes() for o, ln in zip(self.bytes_off[lo:hi].tolist(),
+                                                           self.bytes_len[lo:hi].tolist())]
 
     def __len__(self) -> int:
         return int(self.status.shape[0])
@@ -297,10 +325,7 @@ class BatchResult:
             return self.i64[lo:hi].tolist()
         if kind == 2:
             return self.f32[lo:hi].view(np.float32).tolist()
-        offs = self.bytes_off[lo:hi].tolist()
-        lens = self.bytes_len[lo:hi].tolist()
-        b = self.buf
-        return [b[o : o + ln].tobytes() for o, ln in zip(offs, lens)]
+        return self._bytes_elems(lo, hi)
 
     def record_dict(self, i: int) -> dict:
         """key -> raw feature (reference dict order). Raises the record's exception."""
@@ -376,9 +401,7 @@ class BatchResult:
         elif k == 2:
             vals = self.f32[lo:hi].view(np.float32)
         else:
-            b = self.buf
-            vals = np.array([b[o : o + ln].tobytes() for o, ln in
-                             zip(self.bytes_off[lo:hi].tolist(), self.bytes_len[lo:hi].tolist())], dtype=object)
+            vals = np.array(self._bytes_elems(lo, hi), dtype=object)
         return vals, rs - rs[0]
 
     def crc_ok(self) -> np.ndarray:

@@ -63,6 +63,104 @@ def c3_payloads(n: int = 8192, seed: int = 3, max_len: int = 64) -> list[bytes]:
     return out
 
 
+def c1_blob(n: int, label_offset: int = 0, id_base: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """Vectorised ``c1_payloads``: record i has label (label_offset + i) % 1000 and id
+    f"img-{(id_base + i) % 10**8:08d}". Returns (concatenated payloads, offsets[n + 1]); bytes
+    identical to ``writer.encode_example`` (tests/test_synth.py)."""
+    i = np.arange(n, dtype=np.int64)
+    lab = (label_offset + i) % 1000
+    vl = np.where(lab < 128, 1, 2)
+    rows = np.zeros((n, 43), np.uint8)
+    head = np.frombuffer(b"\x0a\x00\x0a\x00\x0a\x05label\x12\x00\x1a\x00\x0a\x00", np.uint8)
+    rows[:, :17] = head
+    rows[:, 1] = 39 + vl
+    rows[:, 3] = 13 + vl
+    rows[:, 12] = 4 + vl
+    rows[:, 14] = 2 + vl
+    rows[:, 16] = vl
+    rows[:, 17] = np.where(vl == 1, lab, (lab & 0x7F) | 0x80)
+    rows[:, 18] = lab >> 7  # (dropped below for one-byte labels)
+    tail = np.frombuffer(b"\x0a\x16\x0a\x02id\x12\x10\x0a\x0e\x0a\x0cimg-", np.uint8)
+    rows[:, 19:35] = tail
+    x = (id_base + i) % 10**8
+    for k in range(8):
+        rows[:, 42 - k] = 48 + (x // 10**k) % 10
+    keep = np.ones((n, 43), bool)
+    keep[:, 18] = vl == 2
+    blob = rows[keep]
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(41 + vl, out=offs[1:])
+    return blob, offs
+
+
+def frame_blob(blob: np.ndarray, offs: np.ndarray, crc: bool = True) -> np.ndarray:
+    """Frame concatenated payloads (offsets[n + 1]) as TFRecords with the native writer."""
+    from tfr_reader import _native as N
+
+    lib = N.lib()
+    n = offs.shape[0] - 1
+    offs = np.ascontiguousarray(offs, np.uint64)
+    blob = np.ascontiguousarray(blob, np.uint8)
+    total = int(offs[-1]) + 16 * n
+    out = np.empty(max(total, 1), np.uint8)
+    got = lib.tfrg_frame_records(N.ptr(blob if blob.size else np.zeros(1, np.uint8)), N.ptr(offs, N.u64p), n,
+                                 int(crc), N.ptr(out), total)
+    assert got == total
+    return out[:total]
+
+
+# ---------------------------------------------------------------------------------------------
+# C4 (BASELINE.json configs[4], SURVEY §8d D6): a directory of TFRecord files sharded per file over
+# the GPUs. File f draws its record count from default_rng(1000 + f), uniform in +-50 % around the
+# base count, so the LPT partition has real imbalance to absorb.
+# ---------------------------------------------------------------------------------------------
+C4_C1_BASE = 1 << 19  # C1-shaped records per file (~29 MiB): 32 files per GPU ~ 0.92 GiB
+C4_C2_BASE = 256      # C2-shaped (flowers) records per file (~11.7 MB): D6's 128-384
+
+
+def c4_counts(n_files: int, base: int) -> np.ndarray:
+    return np.array([int(base * np.random.default_rng(1000 + f).uniform(0.5, 1.5)) for f in range(n_files)],
+                    np.int64)
+
+
+def c4_file_sizes(n_files: int, shape: str = "c1", base: int | None = None) -> np.ndarray:
+    """Framed byte size of every file of the directory, computed without generating it (C1 shape:
+    57 bytes + a 1-2 byte label varint per record). C2-shaped sizes need the file's random draws."""
+    counts = c4_counts(n_files, base or (C4_C1_BASE if shape == "c1" else C4_C2_BASE))
+    if shape == "c1":
+        per_1000 = 128 * 58 + 872 * 59
+        full, rem = counts // 1000, counts % 1000
+        return full * per_1000 + rem * 58 + np.maximum(rem - 128, 0)
+    return np.array([c4_file(f, "c2", base).size for f in range(n_files)], np.int64)
+
+
+def c4_file(f: int, shape: str = "c1", base: int | None = None, crc: bool = True) -> np.ndarray:
+    """Framed image of file f of the C4 directory (deterministic in f)."""
+    n = int(c4_counts(f + 1, base or (C4_C1_BASE if shape == "c1" else C4_C2_BASE))[f])
+    if shape == "c1":
+        blob, offs = c1_blob(n, 0, f * 1_000_003)
+        return frame_blob(blob, offs, crc)
+    buf, _, _ = framed(c2_payloads(n, seed=1000 + f), crc)
+    return buf
+
+
+def c4_file_name(f: int) -> str:
+    return f"part-{f:05d}.tfrecord"
+
+
+def write_c4_dir(path, n_files: int, shape: str = "c1", base: int | None = None, crc: bool = True) -> list[str]:
+    from pathlib import Path
+
+    d = Path(path)
+    d.mkdir(parents=True, exist_ok=True)
+    out = []
+    for f in range(n_files):
+        p = d / c4_file_name(f)
+        c4_file(f, shape, base, crc).tofile(p)
+        out.append(str(p))
+    return out
+
+
 def framed(payloads: list[bytes], crc: bool = True) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Framed TFRecord image + (start, end) per record."""
     buf = np.frombuffer(writer.frame_records(payloads, crc), np.uint8)
