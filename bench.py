@@ -277,13 +277,15 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> 
     present_small = int(present * n_small / max(n, 1))
     n_tiles = (n + 255) // 256
     alg = {
+        # lane kernel: its records' framed bytes + offsets in; status, verdict, order + count per slot
+        # and a location / single-value word per present list out
         "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
-        "k_slow_count": 0,
-        "k_big_crc": big_bytes + 16 * n_big,
+        # payload CRC of the records above lane_max (the slow list is empty on these workloads)
+        "k_tail_count": big_bytes + 16 * n_big,
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
-        "k_list_gather": vals,
-        "k_wave_gather": vals,
+        # out-of-line lists: every value written once (their record bytes are counted by the lanes)
+        "k_tail_gather": vals,
     }
     a_bytes = alg.get(dominant, framed + 20 * n)
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9

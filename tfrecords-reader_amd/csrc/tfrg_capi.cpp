@@ -76,6 +76,7 @@ struct tfrg_ctx {
   DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum;
   DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
   bool materialized = false;
+  bool tsum_dirty = true;  // the scan words must be cleared before the next decode
   // last batch
   uint32_t n = 0;
   uint64_t cap_hint = 0;  // tfrg_decode_host: total bytes of the given ranges (>= nbytes when they overlap)
@@ -320,6 +321,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
               c->slow_list.cap < nn * 4 || c->tsum.cap < tsum_words * 4 + 16;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  const size_t tsum_cap0 = c->tsum.cap;
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
       c->count.ensure(S * nn * 4) || c->loc.ensure(S * nn * 8) || c->rs.ensure(S * (nn + 1) * 4) ||
       c->slot_base.ensure((S + 1) * 8) || c->totals.ensure((S + 1) * 4) || c->kind_totals.ensure(32) ||
@@ -332,8 +334,12 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   }
   // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
   HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
-  HIP_TRY(hipMemsetD32Async((hipDeviceptr_t)(c->info.as<uint32_t>() + kInfoFirstError), 0xffffffffu, 1, st));
-  if (S && n) HIP_TRY(hipMemsetAsync(c->tsum.p, 0, tsum_words * 4, st));
+  // the row-split scan words are zero between decodes (k_down_gather clears what it used): only a
+  // fresh buffer, or one a failed launch may have left dirty, is cleared here
+  if (c->tsum.cap != tsum_cap0 || c->tsum_dirty) {
+    HIP_TRY(hipMemsetAsync(c->tsum.p, 0, c->tsum.cap, st));
+    c->tsum_dirty = false;
+  }
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
   const bool mat = (flags & TFRG_FLAG_MATERIALIZE_BYTES) != 0;
   const uint64_t lb_words = materialize_lb_words(cap_b);
@@ -427,6 +433,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
     }
     if (ev && e == hipSuccess) e = hipEventRecord(ev[kNumStages], st);
     if (e != hipSuccess) {
+      c->tsum_dirty = true;
       set_error(std::string("kernel launch: ") + hipGetErrorString(e));
       return TFRG_E_HIP;
     }
@@ -487,7 +494,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->n_records = c->n;
   info->n_slots = c->n_slots;
   info->n_errors = h[kInfoErrors];
-  info->first_error = h[kInfoFirstError];
+  info->first_error = ~h[kInfoFirstError];  // (stored inverted by atomicMax; 0 = no error -> 0xffffffff)
   info->n_miss_records = h[kInfoMissRecords];
   info->n_miss_entries = h[kInfoMissEntries];
   info->n_big = h[kInfoBig] + h[kInfoHuge];

@@ -61,7 +61,7 @@ struct DevBatch {
 // Info counters (device, zeroed per decode)
 enum InfoIdx : uint32_t {
   kInfoErrors = 0,       // records with a decode error (reference exception / UB status)
-  kInfoFirstError = 1,   // lowest record index with an error (atomicMin, init 0xffffffff)
+  kInfoFirstError = 1,   // ~(lowest record index with an error): atomicMax of ~r, init 0
   kInfoMissRecords = 2,  // records with a schema miss
   kInfoMissEntries = 3,  // miss entries appended (may exceed capacity)
   kInfoBig = 4,          // records routed to the wave-per-record kernels
@@ -76,6 +76,11 @@ enum InfoIdx : uint32_t {
   kInfoBytesBig = 13,    // k_bytes_scan: long elements listed for the wave copy
   kInfoCount = 16
 };
+
+// verdict byte of a record the lane kernel left to the exact walker (k_tail_count role 1 writes its
+// final verdict, payload CRC included); role 2 (payload CRCs of large records) skips such records,
+// so the two roles of one launch never write the same verdict byte
+constexpr uint32_t kVerdictPending = 0x80u;
 
 // count column: bit 31 set = the slot's single value is stored inline in the loc word
 constexpr uint32_t kCountInline = 0x80000000u;
@@ -153,8 +158,8 @@ struct LaunchCfg {
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageSlowCount, kStageWaveCount, kStageSpine, kStageDownGather,
-                   kStageListGather, kStageWaveGather, kStageMaterialize, kNumStages };
+enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageSpine, kStageDownGather, kStageTailGather,
+                   kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

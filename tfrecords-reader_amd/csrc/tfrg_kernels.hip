@@ -20,6 +20,7 @@
 // The canonical walker and the exact walker share the count/gather sinks, so both paths produce
 // identical columns (tests/test_gpu_parity.py forces each path on the same inputs).
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <type_traits>
 #include "tfrg_internal.h"
 #include "crc32c.h"
@@ -676,7 +677,7 @@ __device__ __forceinline__ void record_result(const DevOut& o, uint32_t r, int s
     atomicAdd(&o.info[kInfoMissRecords], 1u);
   } else if (status != TFRG_OK) {
     atomicAdd(&o.info[kInfoErrors], 1u);
-    atomicMin(&o.info[kInfoFirstError], r);
+    atomicMax(&o.info[kInfoFirstError], ~r);  // stored inverted: zero-initialised with the rest
   }
 }
 
@@ -1489,7 +1490,10 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       uint32_t b0 = 0;
       if (lane == (uint32_t)__builtin_ctzll(sm)) b0 = atomicAdd(&o.info[kInfoSlow], (uint32_t)__popcll(sm));
       b0 = __shfl(b0, __builtin_ctzll(sm), 64);
-      if (slow) o.slow_list[b0 + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = r;
+      if (slow) {
+        o.slow_list[b0 + (uint32_t)__popcll(sm & ((1ull << lane) - 1ull))] = r;
+        o.verdict[r] = (uint8_t)kVerdictPending;
+      }
     }
     if (done) {
       o.status[r] = TFRG_OK;
@@ -1536,8 +1540,8 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
 // Exact reference walk (decoder.pyx:107-300 in its own level-by-level error precedence), one lane per
 // record of the slow list, reading the record from HBM; also the framing errors and schema misses.
 template <int R, bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
+__device__ void role_slow_count(const DevBatch& B, const DevSchema& sc, const DevOut& o,
+                                const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t nslow = o.info[kInfoSlow];
   if (blockIdx.x * kLaneBlock >= nslow) return;  // block-uniform
@@ -1557,14 +1561,15 @@ __global__ __launch_bounds__(kLaneBlock) void k_slow_count(DevBatch B, DevSchema
     if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
     int status = v.status;
     if (status == TFRG_OK) {
-      frame_verdicts<R, false>(B, v, T, nullptr, 0, v.e - v.st <= lane_max);  // larger: k_wave_count
+      // (the payload CRC of a large record too: role 2 skips the records of this role)
+      frame_verdicts<R, false>(B, v, T, nullptr, 0, true);
       sink.reset();
       Src s;
       s.init(B.bytes, v.p0, v.L);
       status = walk_example<COMPAT>(s, sink, aux);
       if (sink.miss) status = TFRG_ST_SCHEMA_MISS;
-      if (status == TFRG_OK && !strict_pass(B, v.verdict, v.e - v.st <= lane_max)) {
-        status = TFRG_ERR_CRC;  // (records above lane_max: their payload CRC is k_big_crc's)
+      if (status == TFRG_OK && !strict_pass(B, v.verdict, true)) {
+        status = TFRG_ERR_CRC;
         aux = v.verdict;
       }
     }
@@ -1737,7 +1742,7 @@ __device__ void strict_reject(const DevOut& o, uint32_t n, uint32_t n_slots, uin
     o.status[r] = TFRG_ERR_CRC;
     o.aux[r] = verdict;
     atomicAdd(&o.info[kInfoErrors], 1u);
-    atomicMin(&o.info[kInfoFirstError], r);
+    atomicMax(&o.info[kInfoFirstError], ~r);  // stored inverted: zero-initialised with the rest
   }
 }
 
@@ -1747,8 +1752,8 @@ __device__ __forceinline__ void set_data_crc(const DevBatch& B, const DevOut& o,
   if ((B.flags & kFlagStrictCrc) && o.status[r] == TFRG_ERR_CRC) o.aux[r] |= TFRG_V_DATA_CRC;
 }
 
-__global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, const uint32_t* __restrict__ crc_tab,
-                                                       const uint32_t* __restrict__ consts, uint32_t n_slots) {
+__device__ void role_big_crc(const DevBatch& B, const DevOut& o, const uint32_t* __restrict__ crc_tab,
+                             const uint32_t* __restrict__ consts, uint32_t n_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   uint32_t* tab = lds;           // [4][256] slice-by-4
   uint32_t* A1 = lds + 1024;     // [4][256] (x) x^8192
@@ -1768,7 +1773,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
   for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
     const uint32_t r = o.big_list[i];
     const RecView v = rec_view(B, r);
-    if (v.e - v.st < 16) continue;
+    const uint32_t pend = __builtin_amdgcn_readfirstlane((uint32_t)o.verdict[r]) & kVerdictPending;
+    if (v.e - v.st < 16 || pend) continue;  // (wave-uniform) role 1's record
     const uint64_t a = v.p0, b = v.e - 4;
     const uint32_t c = b - a >= 64 ? crc_one_wave(B.bytes, a, b, T, A1, cst, lane) : crc_serial<1>(B.bytes, a, b, T);
     const bool good = crc_mask(c) == load_u32_unaligned(B.bytes, b);
@@ -1780,7 +1786,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     PHASE_MARK(h0);
     const uint32_t r = o.big_list[B.n - 1u - i];
     const RecView v = rec_view(B, r);
-    if (v.e - v.st < 16) continue;  // no payload CRC (lane_max below the framing size)
+    // no payload CRC (lane_max below the framing size), or role 1's record (workgroup-uniform: a
+    // thread may read role 1's final verdict while another still reads the marker)
+    const int pend = __syncthreads_or((o.verdict[r] & kVerdictPending) != 0);
+    if (v.e - v.st < 16 || pend) continue;
     const uint64_t a = v.p0, b = v.e - 4;
     uint32_t c;
     if (b - a >= 64) {
@@ -1802,6 +1811,20 @@ __global__ __launch_bounds__(kWaveBlock) void k_big_crc(DevBatch B, DevOut o, co
     PHASE_MARK(h1);
     if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
   }
+}
+
+// The exception paths before the row-split scan in ONE launch (usually both empty): the exact walker
+// for the slow list (role 1), then the payload CRC of records above lane_max (role 2). Strict CRC
+// mode launches them separately (roles 1, then 2), because a strict rejection in role 2 reads the
+// status role 1 wrote for the same record.
+template <bool COMPAT, bool GORD>
+__global__ __launch_bounds__(kLaneBlock) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
+                                                           const uint32_t* __restrict__ crc_tab,
+                                                           const uint32_t* __restrict__ consts, uint32_t lane_max,
+                                                           uint32_t roles) {
+  if (roles & 1u) role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
+  if (roles == 3u) __syncthreads();  // the LDS tables are reloaded by role 2
+  if (roles & 2u) role_big_crc(B, o, crc_tab, consts, sc.n_slots);
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in
@@ -2177,15 +2200,24 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
       if (nd) o.slow_list[b0 + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull))] = r[t];
     }
   }
+  // Leave the scan words zeroed for the next decode (no per-call memset): this workgroup's tile
+  // prefixes of every slot (+ the stride padding after the last tile), and the spine's look-back
+  // words (workgroup 0; k_spine has finished).
+  __syncthreads();
+  const uint32_t t_end = tile0 + kDT < n_tiles ? tile0 + kDT : (tile0 < n_tiles ? o.tile_stride : tile0);
+  const uint32_t span = t_end - tile0;
+  for (uint32_t i = threadIdx.x; i < S * span; i += kLaneBlock)
+    o.tsum[(size_t)(i / span) * o.tile_stride + tile0 + i % span] = 0u;
+  if (blockIdx.x == 0)
+    for (uint32_t i = threadIdx.x; i < 2u * S * o.n_chunks; i += kLaneBlock) reinterpret_cast<uint32_t*>(o.spine_lb)[i] = 0u;
 }
 
 // Out-of-line lists of lane records (k_down_gather's list; lane order within a wave, so the records
 // of a wave are usually one contiguous span): staged in LDS and decoded by their own lane.
 template <bool COMPAT>
-__global__ __launch_bounds__(kLaneBlock) void k_list_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+__device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t lane_max,
+                                 uint8_t* stage) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kStageStride;
   const uint32_t nneed = o.info[kInfoNeed];
   const uint32_t S = sc.n_slots;
   for (uint32_t base = blockIdx.x * kLaneBlock + wib * 64u; base < nneed; base += gridDim.x * kLaneBlock) {
@@ -2232,7 +2264,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_list_gather(DevBatch B, DevSchem
 
 // Huge records: one slot per lane, lists read from HBM.
 template <bool COMPAT>
-__global__ __launch_bounds__(kWaveBlock) void k_wave_gather(DevBatch B, DevSchema sc, DevOut o) {
+__device__ void role_wave_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nhuge = o.info[kInfoHuge];
   for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nhuge; i += gridDim.x * kWavesPerBlock) {
@@ -2442,11 +2474,10 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
 
 // Medium records: staged in LDS with the same register pipeline as k_stage_count.
 template <bool COMPAT>
-__global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSchema sc, DevOut o) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+__device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
   const uint32_t nbig = o.info[kInfoBig];
+  if (blockIdx.x * kWavesPerBlock + wib >= nbig) return;  // wave-uniform: no records for this wave
   const uint32_t stride = gridDim.x * kWavesPerBlock;
   uint32_t i = blockIdx.x * kWavesPerBlock + wib;
   RecPipe q;
@@ -2518,6 +2549,19 @@ __global__ __launch_bounds__(kWaveBlock) void k_stage_gather(DevBatch B, DevSche
   }
 }
 
+// The gathers after the row-split scan in ONE launch, each wave independent (no workgroup barrier):
+// out-of-line lists of lane records (role list), records above lane_max staged in LDS (role stage),
+// huge records from HBM (role wave). Every role uses the wave's stage region of kWStageStride bytes.
+template <bool COMPAT>
+__global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
+  role_list_gather<COMPAT>(B, sc, o, lane_max, stage);
+  role_stage_gather<COMPAT>(B, sc, o, stage);
+  role_wave_gather<COMPAT>(B, sc, o);
+}
+
 // ------------------------------------------------------------------------------------------------
 // launcher
 // ------------------------------------------------------------------------------------------------
@@ -2525,8 +2569,8 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_slow_count",  "k_big_crc",    "k_spine",
-                                             "k_down_gather", "k_list_gather", "k_wave_gather", "k_bytes"};
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_spine",
+                                             "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -2571,23 +2615,23 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
-  mark(kStageSlowCount);
-  // the exception paths (slow records, out-of-line lane lists) are usually empty: a grid of two
-  // workgroups per CU (grid-stride loops) keeps their dispatch cheap
-  const uint32_t tail_grid = (uint32_t)cfg.lane_grid < 2u * (uint32_t)cfg.num_cus ? (uint32_t)cfg.lane_grid
-                                                                                   : 2u * (uint32_t)cfg.num_cus;
-  if (slow_lds <= kLaneLdsBudget) {
-    hipLaunchKernelGGL((k_slow_count<1, COMPAT, false>), dim3(tail_grid), dim3(kLaneBlock), slow_lds, st, b, sc,
-                       o, d_tab, cfg.lane_max);
-  } else {
-    hipLaunchKernelGGL((k_slow_count<1, COMPAT, true>), dim3(tail_grid), dim3(kLaneBlock), 2048ull * 4, st, b,
-                       sc, o, d_tab, cfg.lane_max);
-  }
-  mark(kStageWaveCount);
+  mark(kStageTailCount);
+  // the exception paths before the scan (slow records, payload CRCs of large records) are usually
+  // empty: one launch, grid-stride loops, a workgroup leaves at once when it has nothing to do
   {
+    const bool gord = slow_lds > kLaneLdsBudget;
+    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_lds, (3072 + 128 + 4) * 4);
     const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
-    hipLaunchKernelGGL(k_big_crc, dim3(g), dim3(kWaveBlock), (3072 + 128 + 4) * 4, st, b, o, d_tab, d_consts,
-                       (uint32_t)S);
+    const bool strict = (b.flags & kFlagStrictCrc) != 0;
+    for (uint32_t roles : {strict ? 1u : 3u, strict ? 2u : 0u}) {
+      if (!roles) continue;
+      if (gord)
+        hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab, d_consts,
+                           cfg.lane_max, roles);
+      else
+        hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
+                           d_consts, cfg.lane_max, roles);
+    }
   }
   mark(kStageSpine);
   if (S > 0)
@@ -2601,20 +2645,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles), dim3(kLaneBlock), 0, st, b, sc, o, cfg.lane_max,
                          n_tiles);
   }
-  mark(kStageListGather);
-  if (S > 0)
-    hipLaunchKernelGGL((k_list_gather<COMPAT>), dim3(tail_grid), dim3(kLaneBlock), stage_lds, st, b, sc, o,
-                       cfg.lane_max);
-  mark(kStageWaveGather);
-  if (S > 0) {
+  mark(kStageTailGather);
+  if (S > 0) {  // the gathers after the scan: lane records' lists, staged and huge large records
     const size_t lds = (size_t)kWStageStride * kWavesPerBlock;
-    const void* fn = reinterpret_cast<const void*>(&k_stage_gather<COMPAT>);
+    const void* fn = reinterpret_cast<const void*>(&k_tail_gather<COMPAT>);
     int per_cu = 0;  // one round of resident workgroups (3 per CU: a second round would run at 1/3)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
-    hipLaunchKernelGGL((k_stage_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, sc, o);
-    hipLaunchKernelGGL((k_wave_gather<COMPAT>), dim3(cfg.wave_grid), dim3(kWaveBlock), 0, st, b, sc, o);
+    hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, sc, o, cfg.lane_max);
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)
   return hipGetLastError();
