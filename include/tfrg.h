@@ -62,6 +62,21 @@ int tfrg_index_file(const char* path, uint64_t** out_triples, int64_t* n);
 int tfrg_idx_save(const char* idx_path, const uint64_t* triples, int64_t n);
 int tfrg_idx_load(const char* idx_path, uint64_t** out_triples, int64_t* n);
 void tfrg_free(void* p);
+/* Host staging of a selection (reader.py:212-247 load_records): copies the n byte ranges
+ * [starts[i], ends[i]) of src back to back into dst (NULL: only sizes them); returns the total. */
+uint64_t tfrg_gather_ranges(const uint8_t* src, const uint64_t* starts, const uint64_t* ends, int64_t n,
+                            uint8_t* dst);
+
+/* Compressed TFRecord files (TensorFlow TFRecordOptions "ZLIB" / "GZIP": the whole framed stream
+ * deflated; claimed by the reference's README.md:14, not implemented there). tfrg_compression_of
+ * classifies a file image: an image whose length chain tiles it exactly is uncompressed, else a
+ * gzip / zlib header selects that format. tfrg_inflate decodes either (concatenated gzip members
+ * included) into a malloc'd buffer (free with tfrg_free); the framing index is then built over it. */
+#define TFRG_COMPRESSION_NONE 0
+#define TFRG_COMPRESSION_ZLIB 1
+#define TFRG_COMPRESSION_GZIP 2
+int tfrg_compression_of(const uint8_t* image, uint64_t size);
+int tfrg_inflate(const uint8_t* in, uint64_t size, uint8_t** out, uint64_t* out_len);
 
 /* CRC-32C (Castagnoli) and the TFRecord mask (absent from the reference) */
 uint32_t tfrg_crc32c(const uint8_t* p, uint64_t n);

@@ -166,3 +166,61 @@ def test_load_records_raises_first_error_in_order(tmp_path):
         load_ranges([str(p)] * 3, ptrs[:, 0], ptrs[:, 1])
     feats = load_ranges([str(p)] * 2, ptrs[[0, 2], 0], ptrs[[0, 2], 1])
     assert [f["k"].value for f in feats] == [[1], [1]]
+
+
+@pytest.mark.parametrize("comp", ["GZIP", "ZLIB"])
+def test_compressed_dataset_reads_like_plain(tmp_path, comp):
+    """A directory of ZLIB / GZIP TFRecords (TensorFlow TFRecordOptions): index, random access,
+    load_records and the dataset index all equal to the uncompressed copy's."""
+    from tfr_reader import synth
+
+    plain, packed = tmp_path / "plain", tmp_path / "packed"
+    plain.mkdir()
+    packed.mkdir()
+    for f in range(3):
+        pl = synth.c1_payloads(200 + 50 * f, offset=1000 * f) + _dummy_payloads(3)
+        writer.write_tfrecord(plain / f"p{f}.tfrecord", pl)
+        writer.write_tfrecord(packed / f"p{f}.tfrecord", pl, compression=comp)
+    a = tfr.load_from_directory(plain)
+    b = tfr.load_from_directory(packed, processes=3)
+    assert a.size == b.size == sum(203 + 50 * f for f in range(3))
+    ca = a.index_df[["tfrecord_filename", "tfrecord_start", "tfrecord_end"]].to_numpy().tolist()
+    cb = b.index_df[["tfrecord_filename", "tfrecord_start", "tfrecord_end"]].to_numpy().tolist()
+    assert ca == cb  # offsets into the decompressed stream = the plain file's
+    idx = list(range(0, b.size, 7))
+    assert b[idx] == a[idx]
+    assert b[5] == a[5]
+    _, ea = a.select("SELECT * FROM index WHERE tfrecord_start > 1000")
+    _, eb = b.select("SELECT * FROM index WHERE tfrecord_start > 1000")
+    assert ea == eb and len(ea) > 100
+
+
+def test_columnar_simple_index_equals_per_record(tmp_path):
+    """create_simple_index reads labels from the device columns (SimpleIndexColumns); its rows equal
+    simple_index_fn applied to every decoded Feature (the reference's per-record index_fn), and
+    threaded multi-file indexing (processes=4) equals the serial one."""
+    from tfr_reader import synth
+
+    for f in range(5):
+        writer.write_tfrecord(tmp_path / f"f{f}.tfrecord", synth.c1_payloads(300, offset=300 * f))
+    mapping = {i: {"name": f"class-{i}", "even": i % 2 == 0} for i in range(0, 1000, 3)}
+    default = {"name": "other", "even": None}
+    ds = indexer.create_simple_index(tmp_path, "label", mapping, default, extra_fields=[("id", "image_id")],
+                                     processes=4)
+    fn = indexer.SimpleIndexColumns("label", mapping, default, [("id", "image_id")])
+    serial = indexer.create_index_for_directory(tmp_path, index_fn=lambda f: fn.per_record(f), processes=1)
+    rows = sorted(zip(serial["tfrecord_filename"], serial["tfrecord_start"], serial["label"], serial["name"],
+                      serial["even"], serial["image_id"]))
+    got = sorted(map(tuple, ds[["tfrecord_filename", "tfrecord_start", "label", "name", "even", "image_id"]]
+                     .to_numpy().tolist()))
+    assert [tuple(r) for r in got] == rows and len(rows) == 1500
+    assert rows[0][5].startswith("img-")
+
+
+def test_columnar_index_falls_back_on_missing_key(tmp_path):
+    """A record without the label key: the columnar function defers to the per-record one, which
+    raises the reference's KeyError."""
+    pl = [writer.encode_example([("label", "int64_list", [1])]), writer.encode_example([("x", "int64_list", [2])])]
+    writer.write_tfrecord(tmp_path / "m.tfrecord", pl)
+    with pytest.raises(KeyError, match="not found"):
+        indexer.create_simple_index(tmp_path, "label", {}, {"name": "?"})

@@ -12,6 +12,8 @@
 
 #include <string>
 
+#include <zlib.h>
+
 #include "../../include/tfrg.h"
 #include "crc32c.h"
 
@@ -204,6 +206,99 @@ int tfrg_index_file(const char* path, uint64_t** out_triples, int64_t* n) {
   *out_triples = out;
   *n = cnt;
   return 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Compressed TFRecord files: TensorFlow's TFRecordOptions compression "ZLIB" / "GZIP" deflates the
+// whole framed record stream (the reference's README.md:14 claims support; its code has none).
+// ---------------------------------------------------------------------------------------------
+static bool framing_exact(const uint8_t* img, uint64_t size) {
+  uint64_t pos = 0;
+  while (pos + 8 <= size) {
+    uint64_t len;
+    memcpy(&len, img + pos, 8);
+    if (len > size || pos + 16 + len > size) return false;
+    pos += 16 + len;
+  }
+  return pos == size;
+}
+
+int tfrg_compression_of(const uint8_t* img, uint64_t size) {
+  // a length chain that tiles the file exactly is an uncompressed image, whatever its first bytes
+  if (framing_exact(img, size)) return TFRG_COMPRESSION_NONE;
+  if (size >= 2 && img[0] == 0x1f && img[1] == 0x8b) return TFRG_COMPRESSION_GZIP;
+  if (size >= 2 && (img[0] & 0x0f) == 8 && (img[0] >> 4) <= 7 && (((uint32_t)img[0] << 8) | img[1]) % 31 == 0)
+    return TFRG_COMPRESSION_ZLIB;
+  return TFRG_COMPRESSION_NONE;
+}
+
+int tfrg_inflate(const uint8_t* in, uint64_t size, uint8_t** out, uint64_t* out_len) {
+  *out = nullptr;
+  *out_len = 0;
+  z_stream zs;
+  memset(&zs, 0, sizeof(zs));
+  if (inflateInit2(&zs, 15 + 32) != Z_OK) {  // 15 + 32: zlib or gzip header, detected
+    set_error("inflateInit2 failed");
+    return TFRG_E_IO;
+  }
+  uint64_t cap = size * 4 + 4096, len = 0;
+  uint8_t* buf = (uint8_t*)malloc(cap);
+  const uint8_t* p = in;
+  uint64_t left = size;
+  int rc = Z_OK;
+  while (buf) {
+    if (len == cap) {
+      cap *= 2;
+      uint8_t* nb = (uint8_t*)realloc(buf, cap);
+      if (!nb) {
+        free(buf);
+        buf = nullptr;
+        break;
+      }
+      buf = nb;
+    }
+    const uInt in_chunk = left > (1u << 30) ? (1u << 30) : (uInt)left;
+    const uInt out_chunk = cap - len > (1u << 30) ? (1u << 30) : (uInt)(cap - len);
+    zs.next_in = const_cast<Bytef*>(p);
+    zs.avail_in = in_chunk;
+    zs.next_out = buf + len;
+    zs.avail_out = out_chunk;
+    rc = inflate(&zs, Z_NO_FLUSH);
+    p += in_chunk - zs.avail_in;
+    left -= in_chunk - zs.avail_in;
+    len += out_chunk - zs.avail_out;
+    if (rc == Z_STREAM_END) {
+      // concatenated gzip members (e.g. `cat a.gz b.gz`) decode as one stream
+      if (left >= 2 && p[0] == 0x1f && p[1] == 0x8b && inflateReset(&zs) == Z_OK) continue;
+      break;
+    }
+    if (rc != Z_OK && rc != Z_BUF_ERROR) break;
+    if (rc == Z_BUF_ERROR && left == 0 && len < cap) break;  // truncated input
+  }
+  inflateEnd(&zs);
+  if (!buf) {
+    set_error("out of memory while inflating");
+    return TFRG_E_NOMEM;
+  }
+  if (rc != Z_STREAM_END) {
+    free(buf);
+    set_error(std::string("corrupt or truncated compressed TFRecord stream (zlib: ") + (zs.msg ? zs.msg : "error") + ")");
+    return TFRG_E_IO;
+  }
+  *out = buf;
+  *out_len = len;
+  return 0;
+}
+
+uint64_t tfrg_gather_ranges(const uint8_t* src, const uint64_t* starts, const uint64_t* ends, int64_t n,
+                            uint8_t* dst) {
+  uint64_t at = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const uint64_t len = ends[i] > starts[i] ? ends[i] - starts[i] : 0;
+    if (dst && len) memcpy(dst + at, src + starts[i], len);
+    at += len;
+  }
+  return at;
 }
 
 int tfrg_idx_save(const char* idx_path, const uint64_t* triples, int64_t n) {

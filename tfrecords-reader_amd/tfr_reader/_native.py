@@ -66,7 +66,10 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_idx_save": (C.c_int, [C.c_char_p, u64p, C.c_int64]),
     "tfrg_idx_load": (C.c_int, [C.c_char_p, C.POINTER(u64p), i64p]),
     "tfrg_free": (None, [C.c_void_p]),
+    "tfrg_gather_ranges": (C.c_uint64, [C.c_void_p, u64p, u64p, C.c_int64, C.c_void_p]),
     "tfrg_crc32c": (C.c_uint32, [C.c_void_p, C.c_uint64]),
+    "tfrg_compression_of": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "tfrg_inflate": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(u8p), u64p]),
     "tfrg_masked_crc32c": (C.c_uint32, [C.c_void_p, C.c_uint64]),
     "tfrg_frame_records": (C.c_int64, [C.c_void_p, u64p, C.c_int64, C.c_int, C.c_void_p, C.c_int64]),
     "tfrg_ctx_create": (C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),

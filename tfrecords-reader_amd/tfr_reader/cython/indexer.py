@@ -1,7 +1,8 @@
 """TFRecord framing index and random-access raw reader (reference: cython/indexer.pyx:23-328).
 
 Same contract as the reference ``TFRecordFileReader``: the index is built by a sequential walk of
-the ``[u64 len][u32 crc][payload][u32 crc]`` chain (native, over an mmap: tfrg_index_file), cached
+the ``[u64 len][u32 crc][payload][u32 crc]`` chain (native, over an mmap: tfrg_index_file; over the
+decompressed stream for ZLIB / GZIP files, tfr_reader/_io.py), cached
 next to the file as ``<file>.idx`` (native ``size_t n`` + n x {u64 start, end, size}) and reused
 while its mtime is not older than the file's (indexer.pyx:63-118).
 """
@@ -9,7 +10,6 @@ while its mtime is not older than the file's (indexer.pyx:63-118).
 from __future__ import annotations
 
 import ctypes as C
-import mmap
 import os
 from typing import TypedDict
 
@@ -35,7 +35,12 @@ def _take(ptr: C.POINTER(C.c_uint64), n: int) -> np.ndarray:
 
 
 def create_tfrecord_pointers_index(path: str) -> np.ndarray:
-    """(n, 3) uint64 array of (start, end, example_size) — indexer.pyx:212-252."""
+    """(n, 3) uint64 array of (start, end, example_size) — indexer.pyx:212-252. A compressed
+    (ZLIB / GZIP) file is indexed over its decompressed stream."""
+    from tfr_reader import _io
+
+    if os.path.exists(path) and os.path.getsize(path) and _io.is_compressed(path):
+        return index_buffer(_io.file_image(path))
     out = C.POINTER(C.c_uint64)()
     n = C.c_int64()
     rc = N.lib().tfrg_index_file(path.encode("utf-8"), C.byref(out), C.byref(n))
@@ -82,15 +87,15 @@ class TFRecordFileReader:
     """Random access to the raw records of one TFRecord file."""
 
     def __init__(self, tfrecord_filepath: str, save_index: bool = True):
+        from tfr_reader import _io
+
         self.tfrecord_filepath = tfrecord_filepath
+        if not os.path.exists(tfrecord_filepath):
+            raise OSError(f"Cannot open file: {tfrecord_filepath}")
         self.pointers = self._create_or_load_index(tfrecord_filepath, save_index)
-        try:
-            self._fd = os.open(tfrecord_filepath, os.O_RDONLY)
-        except OSError as e:
-            raise OSError(f"Cannot open file: {tfrecord_filepath}") from e
-        size = os.fstat(self._fd).st_size
-        self._size = size
-        self._map = mmap.mmap(self._fd, size, prot=mmap.PROT_READ) if size else None
+        # the file image: mmap'd, or the decompressed stream of a ZLIB / GZIP file
+        self._img = _io.file_image(tfrecord_filepath)
+        self._size = int(self._img.size)
 
     @staticmethod
     def _create_or_load_index(path: str, save_index: bool) -> np.ndarray:
@@ -131,29 +136,21 @@ class TFRecordFileReader:
         """Raw payload bytes of record idx (length and CRC fields stripped, indexer.pyx:134-193)."""
         if idx < 0 or idx >= len(self):
             raise IndexError("Index out of bounds")
-        if self._map is None and self._fd is None:
+        if self._img is None:
             raise OSError("File is closed")
         start, _end, size = self.pointers[idx].tolist()
         a = start + 12
         if a + size > self._size:
             raise OSError("Failed to read record data")
-        return self._map[a : a + size] if size else b""
+        return self._img[a : a + size].tobytes() if size else b""
 
     @property
     def buffer(self):
-        """The mmap'd file image (for batched device decode)."""
-        return self._map if self._map is not None else b""
+        """The uncompressed file image (for batched device decode)."""
+        return self._img if self._img is not None else np.zeros(0, np.uint8)
 
     def close(self) -> None:
-        if self._map is not None:
-            try:
-                self._map.close()
-            except BufferError:  # views handed out via .buffer are still alive: GC unmaps later
-                pass
-            self._map = None
-        if self._fd is not None:
-            os.close(self._fd)
-            self._fd = None
+        self._img = None
 
     def __enter__(self):
         return self

@@ -19,7 +19,7 @@ from pathlib import Path
 import numpy as np
 
 from tfr_reader import _frame as F
-from tfr_reader import example, hip, indexer, logging
+from tfr_reader import _io, example, hip, indexer, logging
 
 LOGGER = logging.Logger(__name__)
 
@@ -44,30 +44,28 @@ def _decode_framed_bytes(data: bytes, start: int, end: int) -> example.Feature:
 
 
 class TFRecordFileReader:
-    """Reads single framed records of one TFRecord file by byte offsets (reader.py:18-76)."""
+    """Reads single framed records of one TFRecord file by byte offsets (reader.py:18-76). A
+    ZLIB / GZIP compressed file is read through its decompressed stream (tfr_reader/_io.py)."""
 
     def __init__(self, filepath: str):
         _check_path(filepath)
         self.tfrecord_filepath = filepath
-        self._file = None
+        self._file = None  # the open file's image (mmap / decompressed stream), as reader.py:18-76's handle
 
     def get_example(self, start: int, end: int) -> example.Feature:
         if self._file is None:
             raise OSError("File is not open. Use context manager!")
-        self._file.seek(start)
-        data = self._file.read(end - start)
+        data = self._file[start:end].tobytes() if start < self._file.size else b""
         if not data:
             raise OSError(f"Failed to read data from {(start, end)}!")
         return _decode_framed_bytes(data, start, end)
 
     def _open(self):
         if self._file is None:
-            self._file = open(self.tfrecord_filepath, "rb")  # noqa: SIM115
+            self._file = _io.file_image(self.tfrecord_filepath)
 
     def _close(self):
-        if self._file is not None:
-            self._file.close()
-            self._file = None
+        self._file = None
 
     def __enter__(self):
         self._open()
@@ -81,9 +79,14 @@ class TFRecordFileReader:
 def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]) -> list[example.Feature]:
     """Decode framed records given as (file, start, end), in order, in device batches.
 
-    Raises the exception of the first failing record in order, like the reference's ordered
-    ``ThreadPoolExecutor.map`` (reader.py:246-247).
+    Records are grouped by file. A file whose selected bytes are a large part of it is decoded
+    straight from its image (mmap / decompressed stream: no host copy, the ranges index into it);
+    sparser selections are staged back to back by the native gather (tfrg_gather_ranges) into
+    batches of up to MAX_BATCH_BYTES. Raises the exception of the first failing record in order,
+    like the reference's ordered ``ThreadPoolExecutor.map`` (reader.py:246-247).
     """
+    from tfr_reader import _native as N
+
     n = len(paths)
     out: list = [None] * n
     errors: list[BaseException | None] = [None] * n
@@ -92,55 +95,76 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
             with TFRecordFileReader(paths[i]) as r:
                 out[i] = r.get_example(int(starts[i]), int(ends[i]))
         return out
+    starts = np.asarray(starts, np.uint64).reshape(-1)
+    ends = np.asarray(ends, np.uint64).reshape(-1)
     by_file: dict[str, list[int]] = {}
     for i, p in enumerate(paths):
         by_file.setdefault(p, []).append(i)
+    dec = hip.default_decoder()
 
-    pieces: list[np.ndarray] = []
-    b_idx: list[int] = []
-    b_st: list[int] = []
-    b_en: list[int] = []
-    size = 0
-
-    def flush():
-        nonlocal pieces, b_idx, b_st, b_en, size
-        if not b_idx:
+    def take(res, idx: np.ndarray) -> None:
+        il = idx.tolist()
+        if not res.status.any():  # (the usual case: every record decoded, one layout pass)
+            for i, f in zip(il, res.features()):
+                out[i] = f
             return
-        buf = np.concatenate(pieces) if len(pieces) > 1 else pieces[0]
-        res = hip.default_decoder().decode(buf, b_st, b_en)
-        for j, i in enumerate(b_idx):
+        for j, i in enumerate(il):
             e = res.error(j)
             if e is not None:
                 errors[i] = e
             else:
                 out[i] = res.feature(j)
-        pieces, b_idx, b_st, b_en, size = [], [], [], [], 0
+
+    pend_img: list[np.ndarray] = []
+    pend_idx: list[np.ndarray] = []
+    pend_bytes = 0
+
+    def flush() -> None:
+        nonlocal pend_img, pend_idx, pend_bytes
+        if not pend_idx:
+            return
+        idx = np.concatenate(pend_idx)
+        buf = np.empty(pend_bytes, np.uint8)
+        at = 0
+        for img, ii in zip(pend_img, pend_idx):
+            st, en = starts[ii], ends[ii]
+            at += N.lib().tfrg_gather_ranges(N.ptr(img), N.ptr(st, N.u64p), N.ptr(en, N.u64p), st.size,
+                                             N.ptr(buf[at:]) if buf.size else None)
+        lens = (ends[idx] - starts[idx]).astype(np.uint64)
+        b_en = np.cumsum(lens, dtype=np.uint64)
+        take(dec.decode(buf, b_en - lens, b_en), idx)
+        pend_img, pend_idx, pend_bytes = [], [], 0
 
     for path, idxs in by_file.items():
         _check_path(path)
-        with open(path, "rb") as fh:
-            fsize = os.fstat(fh.fileno()).st_size
-            mm = np.memmap(fh, dtype=np.uint8, mode="r") if fsize else np.zeros(0, np.uint8)
-            for i in idxs:
-                s, e = int(starts[i]), int(ends[i])
-                if s >= fsize or e <= s:
-                    errors[i] = OSError(f"Failed to read data from {(s, e)}!")
-                    continue
-                if e > fsize:  # short read: decode alone so its buffer ends where the file does
-                    try:
-                        out[i] = _decode_framed_bytes(bytes(mm[s:fsize]), s, e)
-                    except Exception as exc:  # noqa: BLE001 — re-raised in selection order
-                        errors[i] = exc
-                    continue
-                chunk = np.array(mm[s:e])
-                pieces.append(chunk)
-                b_idx.append(i)
-                b_st.append(size)
-                b_en.append(size + (e - s))
-                size += e - s
-                if size >= MAX_BATCH_BYTES:
-                    flush()
-            del mm
+        img = _io.file_image(path)  # (mmap, or the decompressed stream of a ZLIB / GZIP file)
+        fsize = int(img.size)
+        ii = np.asarray(idxs, np.int64)
+        s, e = starts[ii], ends[ii]
+        bad = (s >= fsize) | (e <= s)
+        for i in ii[bad].tolist():
+            errors[i] = OSError(f"Failed to read data from {(int(starts[i]), int(ends[i]))}!")
+        short = ~bad & (e > fsize)
+        for i in ii[short].tolist():  # short read: decode alone so its buffer ends where the file does
+            try:
+                out[i] = _decode_framed_bytes(img[int(starts[i]) : fsize].tobytes(), int(starts[i]), int(ends[i]))
+            except Exception as exc:  # noqa: BLE001 — re-raised in selection order
+                errors[i] = exc
+        ok = ii[~bad & ~short]
+        if not ok.size:
+            continue
+        sel = int((ends[ok] - starts[ok]).sum())
+        if sel * 4 >= fsize and fsize <= MAX_BATCH_BYTES:  # dense selection: the image itself
+            take(dec.decode(img, starts[ok], ends[ok]), ok)
+            continue
+        for lo in range(0, ok.size, 1 << 20):  # sparse selection: staged back to back
+            part = ok[lo : lo + (1 << 20)]
+            nb = int((ends[part] - starts[part]).sum())
+            if pend_bytes + nb > MAX_BATCH_BYTES:
+                flush()
+            pend_img.append(img)
+            pend_idx.append(part)
+            pend_bytes += nb
     flush()
     for i in range(n):
         if errors[i] is not None:
@@ -168,6 +192,7 @@ class TFRecordDatasetReader:
             index_df = self._load_or_cache_index(index_path)
         self.index_df = F.with_row_index(index_df, "_row_id")
         self._sql = None
+        self._cols = None  # (paths, file index per row, starts, ends), built on first access
         self.logger.info(f"Loaded dataset index with N={F.height(self.index_df)} records ...")
 
     @property
@@ -200,15 +225,17 @@ class TFRecordDatasetReader:
         F.write_parquet(ds, Path(dataset_dir) / indexer.INDEX_FILENAME)
         return cls(str(dataset_dir), index_df=ds, index_cache_dir=index_cache_dir)
 
-    def _rows(self, idxs: list[int]) -> tuple[list[str], list[int], list[int]]:
-        cols = ("tfrecord_filename", "tfrecord_start", "tfrecord_end")
-        paths, starts, ends = [], [], []
-        for i in idxs:
-            r = F.row(self.index_df, i)
-            paths.append(join_path(self.dataset_dir, r[cols[0]]))
-            starts.append(int(r[cols[1]]))
-            ends.append(int(r[cols[2]]))
-        return paths, starts, ends
+    def _rows(self, idxs: list[int]) -> tuple[list[str], np.ndarray, np.ndarray]:
+        """(path, start, end) of index rows, from column arrays taken once (no per-row frame access)."""
+        if self._cols is None:
+            c = F.columns(self.index_df, ["tfrecord_filename", "tfrecord_start", "tfrecord_end"])
+            names = np.asarray(c["tfrecord_filename"], dtype=object)
+            uniq, inv = np.unique(names, return_inverse=True)
+            self._cols = ([join_path(self.dataset_dir, u) for u in uniq.tolist()], inv,
+                          np.asarray(c["tfrecord_start"], np.uint64), np.asarray(c["tfrecord_end"], np.uint64))
+        files, inv, st, en = self._cols
+        ii = np.asarray(idxs, np.int64)
+        return [files[k] for k in inv[ii].tolist()], st[ii], en[ii]
 
     def __getitem__(self, idx):
         if isinstance(idx, Iterable):
@@ -223,7 +250,7 @@ class TFRecordDatasetReader:
             raise IndexError(f"Index {idx=} out of bounds, dataset size={self.size}")
         paths, starts, ends = self._rows([int(idx)])
         with TFRecordFileReader(paths[0]) as reader:
-            return reader.get_example(starts[0], ends[0])
+            return reader.get_example(int(starts[0]), int(ends[0]))
 
     def select(self, sql_query: str):
         selection = self.ctx.execute(sql_query)
@@ -269,16 +296,15 @@ def inspect_dataset_example(dataset_dir: str, filepattern: str = "*.tfrecord"):
     paths = [os.path.join(dataset_dir, p) for p in os.listdir(dataset_dir)]
     paths = sorted(p for p in paths if fnmatch.fnmatch(p, filepattern))
     LOGGER.info("Found N=%s TFRecord files ...", len(paths))
-    with open(paths[0], "rb") as f:
-        length_bytes = f.read(8)
-        if not length_bytes:
-            raise IndexError("Failed to read length bytes")
-        length = struct.unpack("<Q", length_bytes)[0]
-        f.read(4)
-        data = f.read(length)
-        if not data or len(data) < length:
-            raise OSError("Failed to read data!")
-        feature = example.decode(data)
+    img = _io.file_image(paths[0])  # (the decompressed stream of a ZLIB / GZIP file)
+    length_bytes = img[:8].tobytes()
+    if not length_bytes:
+        raise IndexError("Failed to read length bytes")
+    length = struct.unpack("<Q", length_bytes)[0]
+    data = img[12 : 12 + length].tobytes()
+    if not data or len(data) < length:
+        raise OSError("Failed to read data!")
+    feature = example.decode(data)
     info = [
         {"key": k, "type": feature.feature[k].WhichOneof("kind"), "length": len(feature[k].value)}
         for k in list(feature.feature)

@@ -79,7 +79,9 @@ class ShardBatch:
 
 def read_shard(paths: Sequence[str]) -> ShardBatch:
     """Load and index the given TFRecord files (their basenames name them)."""
-    imgs = [np.fromfile(p, dtype=np.uint8) for p in paths]
+    from tfr_reader import _io
+
+    imgs = [_io.file_image(p) for p in paths]  # (decompressed streams of ZLIB / GZIP files)
     return ShardBatch([os.path.basename(p) for p in paths], imgs)
 
 

@@ -64,9 +64,21 @@ def frame_records(payloads: Sequence[bytes], crc: bool = True) -> bytes:
     return out[:total].tobytes()
 
 
-def write_tfrecord(path, payloads: Sequence[bytes], crc: bool = True) -> None:
+def compress(framed: bytes, compression: str | None) -> bytes:
+    """TensorFlow TFRecordOptions compression of a framed stream: "ZLIB" (zlib container) or
+    "GZIP" (gzip container); None leaves it uncompressed."""
+    import zlib
+
+    if not compression:
+        return framed
+    wbits = {"ZLIB": 15, "GZIP": 31}[compression.upper()]
+    c = zlib.compressobj(6, zlib.DEFLATED, wbits)
+    return c.compress(framed) + c.flush()
+
+
+def write_tfrecord(path, payloads: Sequence[bytes], crc: bool = True, compression: str | None = None) -> None:
     with open(path, "wb") as f:
-        f.write(frame_records(payloads, crc))
+        f.write(compress(frame_records(payloads, crc), compression))
 
 
 def masked_crc32c(data: bytes) -> int:
