@@ -171,6 +171,41 @@ int tfrg_result_device(tfrg_ctx* ctx, tfrg_columns* cols);
 /* copy the last result into caller host buffers sized from tfrg_info; NULL members are skipped */
 int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);
 
+/* ---------------------------------------------------------------------------------------------
+ * Double-buffered host -> HBM decode stream (replaces reader.py:212-247's per-record ThreadPool
+ * read+decode for whole-dataset reads). Two slots, each with a pinned staging buffer of batch_bytes,
+ * a device input buffer and its own decode context + stream. tfrg_stream_submit hands a batch (pieces:
+ * file byte ranges or host memory, whole files or record-aligned runs of them) to the slot's worker
+ * thread, which reads / copies it into the slot's pinned buffer (copy_threads threads), indexes every piece with the native framing walk,
+ * enqueues the H2D copies and tfrg_decode_device on the slot's stream, and returns at once; so the
+ * next batch stages while this one decodes. tfrg_stream_wait blocks until the slot's batch is
+ * enqueued and gives its record count (and records per piece); results are then read from
+ * tfrg_stream_ctx(slot) with tfrg_result_info / _fetch / _device and stay valid until the next
+ * submit to that slot. The pieces' memory must stay valid until tfrg_stream_wait returns. Set the
+ * key table on both contexts (tfrg_set_schema) while their slots are idle.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct tfrg_stream tfrg_stream;
+int tfrg_stream_create(int device, uint64_t batch_bytes, int copy_threads, tfrg_stream** out);
+int tfrg_stream_destroy(tfrg_stream* s);
+tfrg_ctx* tfrg_stream_ctx(tfrg_stream* s, int slot);
+/* piece i: bytes [offsets[i], offsets[i] + sizes[i]) of file paths[i] (read with pread), or, where
+ * paths is NULL or paths[i] is NULL, sizes[i] bytes of host memory at pieces[i] (e.g. the
+ * decompressed stream of a ZLIB / GZIP file) */
+int tfrg_stream_submit(tfrg_stream* s, int slot, const uint8_t* const* pieces, const char* const* paths,
+                       const uint64_t* offsets, const uint64_t* sizes, int n_pieces, uint32_t flags);
+/* stage_ms (NULL or 4 doubles): the batch's phases in ms, for the end-to-end report: file read /
+ * copy into pinned memory, framing index, H2D + decode (synchronised), D2H of the columns */
+int tfrg_stream_wait(tfrg_stream* s, int slot, uint64_t* n_records, uint64_t* nbytes, uint64_t* piece_records,
+                     int cap, double* stage_ms);
+/* the slot's decode summary and its result columns, already copied into pinned host memory by the
+ * slot's worker (NULL members: aux when no record failed, bytes_off when bytes are materialised);
+ * valid until the next submit to the slot. A summary with n_miss_records != 0 needs the key table
+ * extended and the batch decoded again (tfrg_decode_host on the slot's context). */
+int tfrg_stream_result(tfrg_stream* s, int slot, tfrg_info* info, tfrg_columns* host);
+/* the slot's pinned copy of its batch (bytes_list views index into it) and its record ranges */
+const uint8_t* tfrg_stream_host_buffer(tfrg_stream* s, int slot);
+int tfrg_stream_host_ranges(tfrg_stream* s, int slot, const uint64_t** starts, const uint64_t** ends);
+
 /* Measurement helper (achievable HBM read bandwidth next to the 8 TB/s spec): one
  * streaming read of d_bytes[0, nbytes) (16 B loads, nbytes a multiple of 16) on `stream`, XOR-folded
  * into the u32 at d_sink so the loads are live. Not part of the decode path. */

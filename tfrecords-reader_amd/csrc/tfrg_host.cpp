@@ -224,12 +224,14 @@ static bool framing_exact(const uint8_t* img, uint64_t size) {
 }
 
 int tfrg_compression_of(const uint8_t* img, uint64_t size) {
-  // a length chain that tiles the file exactly is an uncompressed image, whatever its first bytes
-  if (framing_exact(img, size)) return TFRG_COMPRESSION_NONE;
-  if (size >= 2 && img[0] == 0x1f && img[1] == 0x8b) return TFRG_COMPRESSION_GZIP;
-  if (size >= 2 && (img[0] & 0x0f) == 8 && (img[0] >> 4) <= 7 && (((uint32_t)img[0] << 8) | img[1]) % 31 == 0)
-    return TFRG_COMPRESSION_ZLIB;
-  return TFRG_COMPRESSION_NONE;
+  int kind = TFRG_COMPRESSION_NONE;
+  if (size >= 2 && img[0] == 0x1f && img[1] == 0x8b) kind = TFRG_COMPRESSION_GZIP;
+  else if (size >= 2 && (img[0] & 0x0f) == 8 && (img[0] >> 4) <= 7 && (((uint32_t)img[0] << 8) | img[1]) % 31 == 0)
+    kind = TFRG_COMPRESSION_ZLIB;
+  // a header that looks compressed may still be the start of a plain image (a first record of
+  // length 0x..9c78 begins 78 9c): a length chain that tiles the file exactly means uncompressed
+  if (kind != TFRG_COMPRESSION_NONE && framing_exact(img, size)) kind = TFRG_COMPRESSION_NONE;
+  return kind;
 }
 
 int tfrg_inflate(const uint8_t* in, uint64_t size, uint8_t** out, uint64_t* out_len) {

@@ -70,7 +70,7 @@ def file_image(path: str) -> np.ndarray:
             _CACHE.move_to_end(key)
             return hit
     img = _mmap(path)
-    if compression_of(img) == NONE:
+    if not _header_candidate(img[:2].tobytes()) or compression_of(img) == NONE:
         return img
     out = inflate(img)
     out.setflags(write=False)
@@ -83,5 +83,16 @@ def file_image(path: str) -> np.ndarray:
     return out
 
 
+def _header_candidate(head: bytes) -> bool:
+    """Could these first two bytes open a gzip / zlib stream? (else the file is plain, no walk)"""
+    if len(head) < 2:
+        return False
+    if head[0] == 0x1F and head[1] == 0x8B:
+        return True
+    return (head[0] & 0x0F) == 8 and (head[0] >> 4) <= 7 and ((head[0] << 8) | head[1]) % 31 == 0
+
+
 def is_compressed(path: str) -> bool:
-    return compression_of(_mmap(path)) != NONE
+    with open(path, "rb") as f:
+        head = f.read(2)
+    return _header_candidate(head) and compression_of(_mmap(path)) != NONE

@@ -77,6 +77,15 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_ctx_set_lane_max": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_wave_stage": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "tfrg_stream_create": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
+    "tfrg_stream_destroy": (C.c_int, [C.c_void_p]),
+    "tfrg_stream_ctx": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "tfrg_stream_submit": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_char_p), u64p, u64p,
+                                     C.c_int, C.c_uint32]),
+    "tfrg_stream_wait": (C.c_int, [C.c_void_p, C.c_int, u64p, u64p, u64p, C.c_int, C.POINTER(C.c_double)]),
+    "tfrg_stream_host_buffer": (C.c_void_p, [C.c_void_p, C.c_int]),
+    "tfrg_stream_result": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(TfrgInfo), C.POINTER(TfrgColumns)]),
+    "tfrg_stream_host_ranges": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(u64p), C.POINTER(u64p)]),
     "tfrg_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_profile_last": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
     "tfrg_set_schema": (

@@ -82,10 +82,25 @@ class HipDecoder:
         N.check(self._lib.tfrg_ctx_create(device, C.byref(h)), "tfrg_ctx_create")
         self._ctx = h
 
+    @classmethod
+    def wrap(cls, ctx: int, device: int, keys: KeyTable, spec_varint: bool = False) -> HipDecoder:
+        """A decoder over a context owned elsewhere (a tfrg_stream slot): shares ``keys``, never
+        destroys the context."""
+        d = cls.__new__(cls)
+        d._lib = N.lib()
+        d.device = device
+        d.spec_varint = spec_varint
+        d.keys = keys
+        d._pushed = -1
+        d._lock = threading.Lock()
+        d._ctx = C.c_void_p(ctx)
+        d._owned = False
+        return d
+
     def close(self) -> None:
-        if self._ctx:
+        if self._ctx and getattr(self, "_owned", True):
             self._lib.tfrg_ctx_destroy(self._ctx)
-            self._ctx = None
+        self._ctx = None
 
     def __del__(self):  # noqa: D105
         try:

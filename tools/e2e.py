@@ -1,14 +1,21 @@
 #!/usr/bin/env python3
-"""End-to-end rate: TFRecord file on disk -> Python Feature values.
+"""End-to-end rate, measured in one timed run: TFRecord files on disk -> every value in host memory
+(BASELINE.json north_star).
 
-Stages (timed separately and together): native framing index over the mmap'd file; H2D of the
-file image + device decode + result columns D2H (tfrg_decode_host + fetch); Python Feature
-objects with every value materialised (`.value` of every key, bytes copied out of the mmap).
-usage: e2e.py [--config c1|c2|c3] [--records N]
+The directory is written first (C4 layout: file f of default_rng(1000 + f), C1 / C2 / C3 record
+shapes), then ONE timed pass streams it through ``tfr_reader.stream.StreamDecoder``: mmap of each
+file, native copy into pinned staging (worker threads), native framing index, H2D, device decode
+(framing + CRC-32C + Example decode + columnar gather, bytes_list payloads gathered into a device
+byte column), D2H of every column into numpy arrays. Two slots overlap staging/H2D of batch k+1
+with the decode of batch k. The page cache is warm (the files were just written; dropping it needs
+root): the rate is host memory -> values, not disk -> values. A second figure times turning a
+sample of records into Python ``Feature`` objects with every ``.value`` read (the reference's
+output form).
+
+usage: e2e.py [--config c1|c2|c3] [--files N] [--batch-mib M] [--out PATH]
 """
 import argparse
 import json
-import os
 import sys
 import tempfile
 import time
@@ -19,56 +26,91 @@ sys.path[:0] = [str(REPO / "tfrecords-reader_amd"), str(REPO)]
 
 import numpy as np  # noqa: E402
 
-from tfr_reader import hip, synth, writer  # noqa: E402
-from tfr_reader.cython import indexer as native  # noqa: E402
+from tfr_reader import stream, synth, writer  # noqa: E402
+
+
+def write_dir(d: Path, config: str, n_files: int) -> list[str]:
+    paths = []
+    for f in range(n_files):
+        p = d / f"part-{f:05d}.tfrecord"
+        if config == "c1":
+            synth.c4_file(f, "c1").tofile(p)
+        elif config == "c2":
+            synth.c4_file(f, "c2").tofile(p)
+        else:
+            writer.write_tfrecord(p, synth.c3_payloads(4096, seed=1000 + f))
+        paths.append(str(p))
+    return paths
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="c1")
-    ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--materialize", type=int, default=200000, help="records turned into Python values")
+    ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"])
+    ap.add_argument("--files", type=int, default=None)
+    ap.add_argument("--batch-mib", type=int, default=256)
+    ap.add_argument("--sample", type=int, default=100000, help="records turned into Python Feature values")
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--copy", action="store_true", help="copy each batch's columns out of the pinned buffers")
     a = ap.parse_args()
-    pl = {"c1": lambda: synth.c1_payloads(65536), "c2": lambda: synth.c2_payloads(8189),
-          "c3": lambda: synth.c3_payloads(8192)}[a.config]()
-    reps = {"c1": 16, "c2": 1, "c3": 4}[a.config]
-    with tempfile.TemporaryDirectory(dir="/tmp") as d:
-        path = os.path.join(d, "data.tfrecord")
-        one = writer.frame_records(pl, crc=True)
-        with open(path, "wb") as f:
-            for _ in range(reps):
-                f.write(one)
-        size = os.path.getsize(path)
-        dec = hip.HipDecoder(0)
-        out = {}
-        for it in range(a.reps):
-            t0 = time.perf_counter()
-            reader = native.TFRecordFileReader(path, save_index=False)
-            ptrs = reader.pointers
-            buf = np.frombuffer(reader.buffer, np.uint8)
-            t1 = time.perf_counter()
-            res = dec.decode(buf, ptrs[:, 0], ptrs[:, 1])
-            t2 = time.perf_counter()
-            m = min(a.materialize, len(res))
-            nvals = 0
-            for i in range(m):
-                f = res.feature(i)
-                for k in f.fields_names:
-                    nvals += len(f[k].value)
-            t3 = time.perf_counter()
-            n = len(res)
-            del res, buf
-            reader.close()
-            out = {
-                "config": a.config, "records": n, "file_bytes": size,
-                "index_s": t1 - t0, "index_GiBps": size / (t1 - t0) / 2**30,
-                "decode_host_s": t2 - t1, "decode_host_GiBps": size / (t2 - t1) / 2**30,
-                "decode_host_ex_per_s": n / (t2 - t1),
-                "python_features_per_s": m / (t3 - t2), "python_values": nvals,
-                "end_to_end_GiBps_projected": size / ((t1 - t0) + (t2 - t1) + n / (m / (t3 - t2))) / 2**30,
-                "end_to_end_ex_per_s_projected": n / ((t1 - t0) + (t2 - t1) + n / (m / (t3 - t2))),
-            }
-        print(json.dumps(out))
+    n_files = a.files or {"c1": 16, "c2": 32, "c3": 16}[a.config]
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        paths = write_dir(Path(td), a.config, n_files)
+        file_bytes = sum(Path(p).stat().st_size for p in paths)
+        sd = stream.StreamDecoder(0, batch_bytes=a.batch_mib << 20, copy_threads=8, copy_results=a.copy)
+        # warm-up pass over the whole directory, not timed: device contexts, key learning, and the
+        # pinned result buffers of both slots grown to full batches (steady state)
+        for _ in range(2):  # (the first pass learns the keys: its first batch's results are partial)
+            for b in sd.batches(paths):
+                pass
+        sd.timing = {k: 0.0 for k in sd.timing}
+        t0 = time.perf_counter()
+        n_rec = n_vals = 0
+        stage_ms = np.zeros(4)
+        last = None
+        for b in sd.batches(paths):
+            r = b.result
+            assert not r.status.any()
+            n_rec += len(r)
+            n_vals += int(r.i64.size + r.f32.size + r.bytes_len.size)
+            stage_ms += np.array(b.stage_ms)
+            last = r
+        wall = time.perf_counter() - t0
+        timing = {k: round(v, 4) for k, v in sd.timing.items()}
+        # Python Feature objects with every value read, on a sample of the last batch (its columns
+        # may be views of the stream's pinned buffers: before the stream is closed)
+        k = min(a.sample, len(last))
+        t1 = time.perf_counter()
+        feats = last.features(0, k)
+        nv = 0
+        for f in feats:
+            for key in f.fields_names if hasattr(f, "fields_names") else list(f.feature):
+                nv += len(f[key].value)
+        py_s = time.perf_counter() - t1
+        del feats, last
+        sd.close()
+    out = {
+        "config": a.config,
+        "files": n_files,
+        "file_bytes": file_bytes,
+        "records": n_rec,
+        "values": n_vals,
+        "batch_MiB": a.batch_mib,
+        "wall_s": round(wall, 4),
+        "GiB_s": round(file_bytes / wall / 2**30, 3),
+        "examples_per_s": round(n_rec / wall, 1),
+        "worker_ms": dict(zip(["read_copy", "index", "h2d_decode", "d2h"], np.round(stage_ms, 2).tolist())),
+        "consumer_wait_s": timing,
+        "python_features": {"records": k, "values": nv, "s": round(py_s, 4),
+                            "records_per_s": round(k / py_s, 1)},
+        "copy_results": a.copy,
+        "note": "one timed pass, files on disk in the warm page cache -> every value in host memory: numpy "
+                "columns over the stream's pinned result buffers (copied out with --copy); bytes_list payloads "
+                "gathered on the device and copied back",
+    }
+    line = json.dumps(out)
+    print(line, flush=True)
+    if a.out:
+        Path(a.out).write_text(line + "\n")
 
 
 if __name__ == "__main__":
