@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """HBM traffic per launch of bench.py's dominant kernel from two rocprofv3 PMC passes.
 
-usage (GPU box): pmc_traffic.py <outdir> <config> [kernel-substring]
+usage (GPU box): pmc_traffic.py <outdir> <only> [kernel-substring]
 Runs `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes, MI355X_MICROARCH.md
-§HBM) over `bench.py --config <config> --no-cpu --steps 3 --warmup 1`, keeps the dispatches of the
-kernel over the full batch (largest grid), and writes <outdir>/traffic_<config>.json with the
+§HBM) over `bench.py --only <only> --no-cpu --steps 3 --warmup 1` (<only>: c4, c1file, c2, c3,
+c4c2), keeps the dispatches of the kernel over the full batch (largest grid), and writes
+<outdir>/traffic_<workload>.json (bench.py's workload names: c4_c1, c1file, c2, c3, c4_c2) with the
 per-launch bytes: FETCH_SIZE x 1024 x 2 (gfx950 tallies 128-B fills at 64 B: the guide's correction
 for 16-B-per-lane reads) + WRITE_SIZE x 1024. bench.py reports it as roofline.traffic.
 """
@@ -21,7 +22,7 @@ REPO = Path(__file__).resolve().parents[1]
 def run_pass(out: Path, counter: str, config: str) -> Path:
     d = out / counter
     cmd = ["timeout", "-s", "KILL", "240", "rocprofv3", "--pmc", counter, "--kernel-trace", "--output-format", "csv",
-           "-d", str(d), "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--config", config, "--no-cpu",
+           "-d", str(d), "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--only", config, "--no-cpu",
            "--steps", "3", "--warmup", "1", "--profile-steps", "1"]
     env = dict(os.environ, TMPDIR="/tmp")
     with open(out / f"{counter}.log", "w") as log:
@@ -47,10 +48,11 @@ def main() -> None:
     out.mkdir(parents=True, exist_ok=True)
     name, fetch_kb = per_launch(run_pass(out, "FETCH_SIZE", config), want)
     _, write_kb = per_launch(run_pass(out, "WRITE_SIZE", config), want)
-    res = {"config": config, "kernel": name.split("(")[0], "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+    workload = {"c4": "c4_c1", "c4c2": "c4_c2"}.get(config, config)
+    res = {"config": workload, "kernel": name.split("(")[0], "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
            "traffic_bytes": fetch_kb * 1024 * 2 + write_kb * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 128-B fills tallied at 64 B), WRITE_SIZE as read"}
-    (out / f"traffic_{config}.json").write_text(json.dumps(res, indent=1))
+    (out / f"traffic_{workload}.json").write_text(json.dumps(res, indent=1))
     print(json.dumps(res))
 
 
