@@ -31,7 +31,8 @@ TFRG_HD constexpr uint32_t crc_mask(uint32_t crc) { return ((crc >> 15) | (crc <
 // reflected GF(2) product a (x) b mod P
 TFRG_HD inline uint32_t gf_mul(uint32_t a, uint32_t b) {
   uint32_t p = 0;
-  for (int i = 0; i < 32; ++i) {
+#pragma nounroll
+  for (int i = 0; i < 32; ++i) {  // (a loop: the device kernels call it off their hot paths)
     p ^= (0u - ((a >> 31) & 1u)) & b;  // coefficient of x^i in a (bit 31 - i)
     a <<= 1;
     b = (b >> 1) ^ (kCrcPoly & (0u - (b & 1u)));  // b *= x
@@ -69,11 +70,11 @@ constexpr uint32_t kXInverse = 0x05EC76F1u;  // bit-reverse of 0x8F6E37A0
 // x^(-8z): undoes z trailing zero bytes appended to a message.
 TFRG_HD inline uint32_t gf_xpow8_inv(uint64_t z) { return gf_pow(kXInverse, 8 * z); }
 
-// Byte table for slice-by-4 step tables: T[j][v] = U(0, v followed by j zero bytes)
-// (T[0] is the classic byte table).
-// (8 tables: slice-by-8; the first 4 are the slice-by-4 set)
+// Byte tables T[j][v] = U(0, v followed by j zero bytes) (T[0] is the classic byte table): the
+// first 4 are the slice-by-4 set, 8 slice-by-8, all 16 the slice-by-16 set (one independent
+// lookup per byte of a 16-byte chunk).
 struct CrcTables {
-  uint32_t t[8][256];
+  uint32_t t[16][256];
 };
 
 inline void crc_make_tables(CrcTables* T) {
@@ -84,7 +85,7 @@ inline void crc_make_tables(CrcTables* T) {
   }
   for (uint32_t v = 0; v < 256; ++v) {
     uint32_t c = T->t[0][v];
-    for (int j = 1; j < 8; ++j) {
+    for (int j = 1; j < 16; ++j) {
       c = (c >> 8) ^ T->t[0][c & 0xff];
       T->t[j][v] = c;
     }

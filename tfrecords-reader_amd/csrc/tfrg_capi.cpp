@@ -73,7 +73,7 @@ struct tfrg_ctx {
   DBuf in_bytes, in_start, in_end;
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
-  DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum;
+  DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum, crc_rec, crc_base, crc_part;
   DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
   bool materialized = false;
   bool tsum_dirty = true;  // the scan words must be cleared before the next decode
@@ -110,9 +110,10 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
     set_error("hipStreamCreate failed");
     return TFRG_E_HIP;
   }
-  // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (wavefront kernels), then
-  // [8][256] slice-by-8 (lane kernel); consts: 64 lane shifts x^(128 l) and 16 un-shifts x^(-8z)
-  std::vector<uint32_t> tab(5120), cst(128);
+  // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
+  // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
+  // 32 round shifts x^(8192 * 2^k)
+  std::vector<uint32_t> tab(8192), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -120,11 +121,10 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   crc_make_mul_tables(gf_xpow8(1024), M);
   memcpy(tab.data() + 1024, M, 4096);
   memcpy(tab.data() + 2048, T.t, 8192);
-  crc_make_mul_tables(gf_xpow8(4096), M);  // (x) x^32768: four interleaved waves of 1 KiB rounds
-  memcpy(tab.data() + 4096, M, 4096);
+  memcpy(tab.data() + 4096, T.t, 16384);  // slice-by-16 (streaming CRC)
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
-  for (int w = 0; w < 4; ++w) cst[80 + w] = gf_xpow8(1024ull * w);  // wave w's rounds: x^(8192 w)
+  for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts
   if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||
       hipMemcpy(c->crc_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->consts.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -144,7 +144,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
-                 &c->bdata, &c->boff64, &c->blb, &c->bbig};
+                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part};
   for (DBuf* b : all) b->release();
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
@@ -319,7 +319,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
               c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
-              c->slow_list.cap < nn * 4 || c->tsum.cap < tsum_words * 4 + 16;
+              c->slow_list.cap < nn * 4 || c->tsum.cap < tsum_words * 4 + 16 || c->crc_rec.cap < nn * 4 ||
+              c->crc_base.cap < nn * 8 || c->crc_part.cap < nn * 8;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   const size_t tsum_cap0 = c->tsum.cap;
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
@@ -328,7 +329,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
       c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->slow_list.ensure(nn * 4) ||
       c->miss.ensure(kMissCap * 16ull) || c->info.ensure(kInfoCount * 4) ||
-      c->tsum.ensure(tsum_words * 4 + 16)) {
+      c->tsum.ensure(tsum_words * 4 + 16) || c->crc_rec.ensure(nn * 4) || c->crc_base.ensure(nn * 8) ||
+      c->crc_part.ensure(nn * 8)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
@@ -391,6 +393,9 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.spine_lb = reinterpret_cast<uint64_t*>(o.tsum + (size_t)S * tile_stride);  // 16-byte aligned
   o.n_chunks = n_chunks;
   o.slow_list = c->slow_list.as<uint32_t>();
+  o.crc_rec = c->crc_rec.as<uint32_t>();
+  o.crc_base = c->crc_base.as<uint64_t>();
+  o.crc_part = c->crc_part.as<uint64_t>();
   LaunchCfg cfg;
   cfg.num_cus = c->num_cus;
   const uint64_t lane_blocks = (n + 255) / 256;

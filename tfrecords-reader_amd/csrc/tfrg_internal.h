@@ -74,6 +74,7 @@ enum InfoIdx : uint32_t {
   kInfoOverflow = 11,    // a kind's value total exceeds its column capacity (overlapping ranges)
   kInfoBytesTicket = 12, // k_bytes_scan tile tickets
   kInfoBytesBig = 13,    // k_bytes_scan: long elements listed for the wave copy
+  kInfoCrcCtr = 14,      // [14..15] u64: streaming-CRC list entries << kCrcIdxShift | flat 1 KiB rounds
   kInfoCount = 16
 };
 
@@ -81,6 +82,11 @@ enum InfoIdx : uint32_t {
 // final verdict, payload CRC included); role 2 (payload CRCs of large records) skips such records,
 // so the two roles of one launch never write the same verdict byte
 constexpr uint32_t kVerdictPending = 0x80u;
+
+// streaming payload CRC of the large records (k_tail_count role 2)
+constexpr int kCrcIdxShift = 40;
+constexpr uint64_t kCrcRoundMask = (1ull << kCrcIdxShift) - 1ull;
+constexpr uint32_t kCrcListMin = 64;  // shorter payloads of large records: the lane kernel's serial CRC
 
 // count column: bit 31 set = the slot's single value is stored inline in the loc word
 constexpr uint32_t kCountInline = 0x80000000u;
@@ -112,6 +118,9 @@ struct DevOut {
   uint32_t n_chunks;     // ceil(n_tiles / 2^kSpineChunkShift)
   uint32_t* slow_list;   // [n] lane records for the exact walker; reused by k_down_gather for the
                          // records k_list_gather decodes (the slow list is consumed by then)
+  uint32_t* crc_rec;     // [n] streaming-CRC list: record
+  uint64_t* crc_base;    // [n] its first flat round (ascending with the list index)
+  uint64_t* crc_part;    // [n] rounds done << 32 | XOR of the slices, of a record split over waves
 };
 
 // Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)
@@ -158,7 +167,7 @@ struct LaunchCfg {
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageSpine, kStageDownGather, kStageTailGather,
+enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageCrc, kStageSpine, kStageDownGather, kStageTailGather,
                    kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 

@@ -663,7 +663,7 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
 #ifndef TFRG_LANE_MINB
-#define TFRG_LANE_MINB 4  // workgroups per CU the count kernel is register-budgeted for
+#define TFRG_LANE_MINB 6  // waves per SIMD the (LDS-dict) count kernel is register-budgeted for
 #endif
 constexpr int kWaveBlock = 256;
 constexpr int kWavesPerBlock = kWaveBlock / 64;
@@ -1341,6 +1341,43 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
   return x;
 }
 
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(v, d, 64);
+    if (lane >= (uint32_t)d) v += y;
+  }
+  return v;
+}
+
+// 1 KiB rounds (64 lanes x aligned 16-byte chunks) covering the payload [a, b), b > a
+__device__ __forceinline__ uint32_t crc_rounds_of(uint64_t a, uint64_t b) {
+  return (uint32_t)((((b - 1) >> 4) - (a >> 4) + 64) >> 6);
+}
+
+// Lists this wave's accepted large records (j = their round count, 0 = none) for the streaming
+// payload CRC (k_tail_count role 2). ONE 64-bit atomic per wave returns both the list index and
+// the flat round base, so list order and round order agree: entry i owns the flat rounds
+// [crc_base[i], crc_base[i + 1]).
+__device__ __forceinline__ void crc_list_append(const DevOut& o, uint32_t r, uint32_t j, uint32_t lane) {
+  const uint64_t m = __ballot(j != 0);
+  if (!m) return;
+  const uint32_t incl = wave_incl_scan_u32(j, lane);
+  const uint32_t tot = __shfl(incl, 63, 64);
+  unsigned long long t = 0;
+  if (lane == 0)
+    t = atomicAdd(reinterpret_cast<unsigned long long*>(o.info + kInfoCrcCtr),
+                  ((unsigned long long)__popcll(m) << kCrcIdxShift) | tot);
+  const uint64_t tu = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(t >> 32), 0, 64) << 32) |
+                      (uint32_t)__shfl((int)(uint32_t)t, 0, 64);
+  if (j) {
+    const uint32_t idx = (uint32_t)(tu >> kCrcIdxShift) + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+    o.crc_rec[idx] = r;
+    o.crc_base[idx] = (tu & kCrcRoundMask) + incl - j;
+    o.crc_part[idx] = 0;
+  }
+}
+
 // Wave-uniform values loaded with VECTOR loads: a laundered (VGPR) index keeps the compiler from
 // turning the load into a scalar one, whose lgkmcnt would be drained by every LDS wait of the walk.
 __device__ __forceinline__ uint32_t vgpr_launder(uint32_t x) {
@@ -1362,7 +1399,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 // GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
 // MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
 template <int R, bool COMPAT, int MODE>
-__global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -1473,9 +1510,11 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
     const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));
     if (__ballot(bigw)) {
       if (bigw) {
-        frame_verdicts<R, false>(B, v, T, nullptr, 0, mine);
+        // (the payload CRC of a large record is role 2's stream, unless it is shorter than one round)
+        const bool crc_here = mine || (uint64_t)v.L < kCrcListMin;
+        frame_verdicts<R, false>(B, v, T, nullptr, 0, crc_here);
         sink.fast_reset(S);
-        if (strict_pass(B, v.verdict, mine)) {
+        if (strict_pass(B, v.verdict, crc_here)) {
           const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
           done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
           tried = true;
@@ -1499,6 +1538,10 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       o.status[r] = TFRG_OK;
       o.verdict[r] = (uint8_t)v.verdict;
     }
+    // the payload CRC of an accepted large record: one entry of the streaming CRC list
+    const bool crc_on = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
+    const uint32_t crc_j =
+        done && !mine && crc_on && v.e - v.st >= 16 && (uint64_t)v.L >= kCrcListMin ? crc_rounds_of(v.p0, v.e - 4) : 0u;
     // order / count columns of the accepted records + the tile sums (one atomic per slot and wave)
     const uint32_t tile = (uint32_t)(base >> kTileShift);
     if constexpr (MODE == 1) {
@@ -1530,6 +1573,7 @@ __global__ __launch_bounds__(kLaneBlock, TFRG_LANE_MINB) void k_lane_count(DevBa
       }
     }
     }
+    crc_list_append(o, r, crc_j, lane);
     wave_lds_sync();  // the stage is rewritten by the next iteration
     PHASE_MARK(p5);
     PHASE_ADD(19, p4, p5);
@@ -1627,103 +1671,99 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
   }
 }
 
-#ifndef TFRG_HUGE_DEPTH
-#define TFRG_HUGE_DEPTH 8
+#ifndef TFRG_CRC_DEPTH
+#define TFRG_CRC_DEPTH 4
 #endif
-// Huge records (span beyond the LDS stage): one WORKGROUP per record. The payload CRC is split over
-// the 4 waves by interleaved 1 KiB rounds (64 lanes x 16-byte chunks, rounds counted from the end;
-// wave w takes rounds w, w+4, w+8, ...) with kHugeDepth rounds of loads in flight per lane. A lane's
-// state advances by x^32768 per step of its wave (A4 tables), wave w's lane-combined sum is shifted
-// by x^(8192 w), and the four sums XOR together (crc32c.h algebra). Wave 0 then runs the exact,
-// wave-uniform walk over the (now L2-warm) record.
-constexpr int kHugeDepth = TFRG_HUGE_DEPTH;
+// Streaming payload CRC of the large records (k_tail_count role 2). The lane kernel lists every
+// accepted record above lane_max (crc_list_append) with its 1 KiB rounds counted into ONE flat
+// round space: list entry i owns the flat rounds [base_i, base_{i+1}); round j of a record,
+// counted from its end, is its aligned 16-byte chunks c1 - 64 j - lane. Every wave of the launch
+// takes an equal contiguous slice of the flat space, so the large payloads of a batch stream
+// through the chip with kCrcDepth rounds of loads in flight per wave whatever the record sizes
+// (one record per wave or workgroup left latency chains per record and the load imbalance of
+// lognormal sizes). A lane's state advances by x^8192 per round (Horner, A1 tables); a record's
+// rounds inside one wave are lane-combined (x^(128 l)) and shifted by x^(8192 jlo) to their place;
+// the slices of a record split over waves XOR together in crc_part (CRC-32C is linear, crc32c.h)
+// and the wave whose rounds complete the record finishes it.
+constexpr int kCrcDepth = TFRG_CRC_DEPTH;
+#ifndef TFRG_CRC_WAVES
+#define TFRG_CRC_WAVES 5  // waves per SIMD k_crc_stream is register-budgeted for
+#endif
+constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
+constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
+constexpr uint32_t kNumCst = 128;
 
 // U(0, 16-byte chunk at q) of the payload [a, b): bytes outside zeroed, the first 4 payload bytes
 // inverted (the ~0 initial state)
 __device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uint64_t b, const LdsTab<1>& T) {
   uint32_t ws[4] = {w.x, w.y, w.z, w.w};
   if (q < a + 4 || q + 16 > b) {
+    // chunk-relative byte bounds in [0, 16]: keep [lo, hi), invert [lo, li) (the payload's first 4)
+    const int64_t la = (int64_t)(a - q), lb = (int64_t)(b - q);
+    const uint32_t lo = la <= 0 ? 0u : (la >= 16 ? 16u : (uint32_t)la);
+    const uint32_t hi = lb <= 0 ? 0u : (lb >= 16 ? 16u : (uint32_t)lb);
+    const uint32_t li = la + 4 <= 0 ? 0u : (la + 4 >= 16 ? 16u : (uint32_t)(la + 4));  // end of the first 4
 #pragma unroll
     for (int k2 = 0; k2 < 4; ++k2) {
-      uint32_t keep = 0, inv = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint64_t ba = q + 4ull * k2 + j;
-        if (ba >= a && ba < b) keep |= 0xffu << (8 * j);
-        if (ba >= a && ba < a + 4) inv |= 0xffu << (8 * j);
-      }
+      auto upto = [](uint32_t x, int k) {  // bytes of word k below chunk byte x
+        const uint32_t n = x <= 4u * k ? 0u : (x - 4u * k >= 4u ? 4u : x - 4u * k);
+        return n >= 4u ? 0xffffffffu : (1u << (8u * n)) - 1u;
+      };
+      const uint32_t below_lo = upto(lo, k2);
+      const uint32_t keep = upto(hi, k2) & ~below_lo;
+      const uint32_t inv = upto(li, k2) & ~below_lo & keep;
       ws[k2] = (ws[k2] & keep) ^ inv;
     }
   }
-  uint32_t Rc = 0;
+  // slice-by-16: byte i of the chunk is followed by 15 - i bytes (T holds the 16 tables), so the
+  // 16 lookups are independent (no serial step chain per chunk)
+  uint32_t r0 = 0, r1 = 0;
 #pragma unroll
-  for (int k2 = 0; k2 < 4; ++k2) Rc = T.step4(Rc ^ ws[k2]);
-  return Rc;
+  for (int k2 = 0; k2 < 4; ++k2) {
+    const uint32_t x = ws[k2];
+    r0 ^= T.at4(15 - 4 * k2, byte_x4<0>(x)) ^ T.at4(14 - 4 * k2, byte_x4<1>(x));
+    r1 ^= T.at4(13 - 4 * k2, byte_x4<2>(x)) ^ T.at4(12 - 4 * k2, byte_x4<3>(x));
+  }
+  return r0 ^ r1;
+}
+
+// chunk_u of an interior chunk (no masks) with the slice-by-16 tables at LDS address 0: all 16
+// table reads issued before the one wait (one LDS round trip per chunk; the compiler's schedule
+// drained them in two halves), in a single asm block so that no result is read before the wait.
+// Each read overwrites its own address register (16 VGPRs, not 32).
+__device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
+  uint32_t r0 = byte_x4<0>(w.x), r1 = byte_x4<1>(w.x), r2 = byte_x4<2>(w.x), r3 = byte_x4<3>(w.x);
+  uint32_t r4 = byte_x4<0>(w.y), r5 = byte_x4<1>(w.y), r6 = byte_x4<2>(w.y), r7 = byte_x4<3>(w.y);
+  uint32_t r8 = byte_x4<0>(w.z), r9 = byte_x4<1>(w.z), r10 = byte_x4<2>(w.z), r11 = byte_x4<3>(w.z);
+  uint32_t r12 = byte_x4<0>(w.w), r13 = byte_x4<1>(w.w), r14 = byte_x4<2>(w.w), r15 = byte_x4<3>(w.w);
+  asm volatile(
+      "ds_read_b32 %0, %0 offset:15360\n\t"
+      "ds_read_b32 %1, %1 offset:14336\n\t"
+      "ds_read_b32 %2, %2 offset:13312\n\t"
+      "ds_read_b32 %3, %3 offset:12288\n\t"
+      "ds_read_b32 %4, %4 offset:11264\n\t"
+      "ds_read_b32 %5, %5 offset:10240\n\t"
+      "ds_read_b32 %6, %6 offset:9216\n\t"
+      "ds_read_b32 %7, %7 offset:8192\n\t"
+      "ds_read_b32 %8, %8 offset:7168\n\t"
+      "ds_read_b32 %9, %9 offset:6144\n\t"
+      "ds_read_b32 %10, %10 offset:5120\n\t"
+      "ds_read_b32 %11, %11 offset:4096\n\t"
+      "ds_read_b32 %12, %12 offset:3072\n\t"
+      "ds_read_b32 %13, %13 offset:2048\n\t"
+      "ds_read_b32 %14, %14 offset:1024\n\t"
+      "ds_read_b32 %15, %15\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7), "+v"(r8), "+v"(r9),
+        "+v"(r10), "+v"(r11), "+v"(r12), "+v"(r13), "+v"(r14), "+v"(r15));
+  return ((r0 ^ r1) ^ (r2 ^ r3)) ^ ((r4 ^ r5) ^ (r6 ^ r7)) ^ ((r8 ^ r9) ^ (r10 ^ r11)) ^
+         ((r12 ^ r13) ^ (r14 ^ r15));
 }
 
 __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
   return M[S & 0xffu] ^ M[256 + ((S >> 8) & 0xffu)] ^ M[512 + ((S >> 16) & 0xffu)] ^ M[768 + (S >> 24)];
 }
 
-// Horner over this wave's rounds j = J-1 .. 0, DEPTH rounds of loads in flight
-// (STEP waves share a record: this wave's rounds are w + STEP j, its multiplier A = x^(8192 STEP))
-template <int DEPTH, int STEP>
-__device__ __forceinline__ uint32_t crc_rounds(const uint8_t* buf, uint64_t a, uint64_t b, int64_t c0, int64_t c1,
-                                               int64_t J, const LdsTab<1>& T, const uint32_t* A4, uint32_t w,
-                                               uint32_t lane) {
-  uint32_t S = 0;
-  for (int64_t j = J - 1; j >= 0; j -= DEPTH) {  // from the payload start (largest round)
-    uint4 wv[DEPTH];
-    int64_t chv[DEPTH];
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {  // every load of the group in flight before any use
-      const int64_t k = (int64_t)w + STEP * (j - d);
-      const int64_t ch = c1 - 64 * k - (int64_t)lane;
-      chv[d] = ch;
-      const bool in = j - d >= 0 && ch >= c0;
-      wv[d] = *reinterpret_cast<const uint4*>(buf + (in ? (uint64_t)ch << 4 : (a & ~15ull)));
-    }
-#pragma unroll
-    for (int d = 0; d < DEPTH; ++d) {
-      if (j - d < 0) break;  // wave-uniform
-      const uint32_t Rc = chv[d] >= c0 ? chunk_u(wv[d], (uint64_t)chv[d] << 4, a, b, T) : 0u;
-      S = mul_tab(A4, S) ^ Rc;
-    }
-  }
-  return S;
-}
-
-// this wave's share of U(0, payload') over [a, b) (b - a >= 64), lane-combined, not yet shifted
-__device__ __forceinline__ uint32_t crc_huge_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
-                                                  const uint32_t* A4, const uint32_t* cst, uint32_t w, uint32_t lane) {
-  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
-  const int64_t rounds = (c1 - c0 + 64) >> 6;
-  const int64_t J = rounds > (int64_t)w ? (rounds - (int64_t)w + 3) / 4 : 0;  // rounds w + 4j, j < J
-  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth, 4>(buf, a, b, c0, c1, J, T, A4, w, lane)
-                                     : crc_rounds<2, 4>(buf, a, b, c0, c1, J, T, A4, w, lane);
-  uint32_t t = gf_mul(S, cst[lane]);  // chunk position inside its round: x^(128 l)
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
-  return t;
-}
-
-// CRC-32C of a payload [a, b) (b - a >= 64) by one wave: consecutive 1 KiB rounds, x^8192 per step
-__device__ __forceinline__ uint32_t crc_one_wave(const uint8_t* buf, uint64_t a, uint64_t b, const LdsTab<1>& T,
-                                                 const uint32_t* A1, const uint32_t* cst, uint32_t lane) {
-  const int64_t c0 = (int64_t)(a >> 4), c1 = (int64_t)((b - 1) >> 4);
-  const int64_t J = (c1 - c0 + 64) >> 6;
-  const uint32_t S = J >= kHugeDepth ? crc_rounds<kHugeDepth, 1>(buf, a, b, c0, c1, J, T, A1, 0, lane)
-                                     : crc_rounds<2, 1>(buf, a, b, c0, c1, J, T, A1, 0, lane);
-  uint32_t t = gf_mul(S, cst[lane]);
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t ^= __shfl_xor(t, m, 64);
-  const uint32_t z = (uint32_t)(16ull * (uint64_t)(c1 + 1) - b);
-  return ~gf_mul(t, cst[64 + z]);
-}
-
-// Payload CRC-32C of every record above lane_max (their framing bits and walk are the lane / slow
-// kernels'), the DATA_CRC verdict bit OR-ed into the verdict column. Records whose span fits the
-// wave stage (the front of big_list) take one WAVE each; larger ones one WORKGROUP each.
 // TFRG_FLAG_STRICT_CRC, payload CRC of a record above lane_max failed: the record becomes an error
 // (status TFRG_ERR_CRC, aux = verdict) and its counts are withdrawn from the columns and the tile
 // sums before k_spine scans them. `t` indexes the slots with stride `nt` (the calling wave / group).
@@ -1746,85 +1786,260 @@ __device__ void strict_reject(const DevOut& o, uint32_t n, uint32_t n_slots, uin
   }
 }
 
-// a matching payload CRC; a strict-mode rejection of the slow kernel (length CRC) keeps aux = verdict
-__device__ __forceinline__ void set_data_crc(const DevBatch& B, const DevOut& o, uint32_t r) {
-  o.verdict[r] |= (uint8_t)TFRG_V_DATA_CRC;
-  if ((B.flags & kFlagStrictCrc) && o.status[r] == TFRG_ERR_CRC) o.aux[r] |= TFRG_V_DATA_CRC;
+__device__ __forceinline__ uint64_t rl64(uint64_t x, uint32_t k) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), (int)k) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)k);
+}
+__device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t k) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)k);
 }
 
-__device__ void role_big_crc(const DevBatch& B, const DevOut& o, const uint32_t* __restrict__ crc_tab,
-                             const uint32_t* __restrict__ consts, uint32_t n_slots) {
+// x^(8192 j): the factors x^(8192 * 2^k) of the set bits of j, multiplied across lanes 0..31
+__device__ __forceinline__ uint32_t xpow_rounds(uint32_t j, const uint32_t* cst, uint32_t lane) {
+  uint32_t f = (lane < 32u && ((j >> (lane & 31u)) & 1u)) ? cst[kCstRoundPow + (lane & 31u)] : 0x80000000u;
+#pragma unroll
+  for (int m = 1; m < 32; m <<= 1) f = gf_mul(f, (uint32_t)__shfl_xor((int)f, m, 64));
+  return rfl32(f);
+}
+
+// The streaming-CRC window: lane k < 63 describes list entry win0 + k, lane 63 holds the next
+// window's first flat round (the bound of this one).
+struct CrcWin {
+  uint64_t base;    // first flat round
+  uint64_t E;       // chunk of flat round R, lane l: E + 64 R - l
+  uint64_t c0;      // first payload chunk
+  uint64_t a, b;    // payload [a, b)
+  uint32_t J, r, verdict, stored;
+};
+
+__device__ __forceinline__ CrcWin crc_win_load(const DevBatch& B, const DevOut& o, uint32_t win0, uint32_t nrec,
+                                               uint64_t TR, uint32_t lane) {
+  CrcWin w{};
+  const uint32_t idx = win0 + lane;
+  w.base = idx < nrec ? o.crc_base[idx] : TR;
+  if (idx < nrec && lane < 63u) {
+    w.r = o.crc_rec[idx];
+    const RecView v = rec_view(B, w.r);
+    w.a = v.p0;
+    w.b = v.e - 4;
+    w.verdict = o.verdict[w.r];
+    w.stored = load_u32_unaligned(B.bytes, w.b);
+    const uint64_t c1 = (w.b - 1) >> 4;
+    w.c0 = w.a >> 4;
+    w.J = (uint32_t)((c1 - w.c0 + 64) >> 6);
+    w.E = c1 - 64ull * (w.J - 1u) - 64ull * w.base;
+  }
+  // the window's loads retired here: the group loads issued after it then carry no false wait on
+  // them (a merged loop-header state otherwise drains vmcnt before every group)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  return w;
+}
+
+// the rounds [Rf, Rl] of window entry k, Horner sum S per lane: placed, combined with the other
+// waves' slices of the record, and, once complete, checked against the stored CRC
+__device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, const CrcWin& w, uint32_t win0,
+                                       uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
+                                       uint32_t n_slots, uint32_t lane) {
+  const uint64_t bas = rl64(w.base, k);
+  const uint32_t J = rl32(w.J, k);
+  const uint32_t jtop = J - 1u - (uint32_t)(Rf - bas), jlo = J - 1u - (uint32_t)(Rl - bas);
+  uint32_t t = gf_mul(S, cst[lane]);
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t ^= (uint32_t)__shfl_xor((int)t, m, 64);
+  if (jlo) t = gf_mul(t, xpow_rounds(jlo, cst, lane));
+  if (jlo != 0u || jtop != J - 1u) {  // a slice of a record split over waves
+    // (rounds done << 32 | XOR of the slices) updated in ONE 64-bit compare-and-swap: the wave that
+    // completes the rounds sees every other slice in the value it replaced, with no fence (an
+    // agent-scope fence per slice wrote back and invalidated L2 under the streaming loads)
+    const uint32_t n_r = jtop - jlo + 1u;
+    uint64_t seen = 0;
+    if (lane == 0) {
+      unsigned long long* p = reinterpret_cast<unsigned long long*>(o.crc_part + (win0 + k));
+      unsigned long long cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (;;) {
+        const unsigned long long nv = ((cur >> 32) + n_r) << 32 | (uint32_t)((uint32_t)cur ^ t);
+        const unsigned long long prev = atomicCAS(p, cur, nv);
+        if (prev == cur) break;
+        cur = prev;
+      }
+      seen = cur;
+    }
+    seen = rl64(seen, 0);
+    if ((uint32_t)(seen >> 32) + n_r != J) return;  // another wave finishes the record
+    t ^= (uint32_t)seen;
+  }
+  const uint64_t b = rl64(w.b, k);
+  const uint32_t r = rl32(w.r, k), verdict = rl32(w.verdict, k);
+  const uint32_t z = (uint32_t)(16ull * (((b - 1) >> 4) + 1ull) - b);  // zero bytes padding the last chunk
+  const uint32_t c = ~gf_mul(t, cst[kCstUnshift + z]);
+  if (crc_mask(c) == rl32(w.stored, k)) {
+    if (lane == 0) o.verdict[r] = (uint8_t)(verdict | TFRG_V_DATA_CRC);
+  } else if (B.flags & kFlagStrictCrc) {
+    strict_reject(o, B.n, n_slots, r, verdict, lane, 64);
+  }
+}
+
+__device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut& o, const uint32_t* __restrict__ crc_tab,
+                                const uint32_t* __restrict__ consts, uint32_t n_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  uint32_t* tab = lds;           // [4][256] slice-by-4
-  uint32_t* A1 = lds + 1024;     // [4][256] (x) x^8192
-  uint32_t* A4 = lds + 2048;     // [4][256] (x) x^32768
-  uint32_t* cst = lds + 3072;    // [128] lane shifts x^(128 l), un-shifts x^(-8z), wave shifts x^(8192 w)
-  uint32_t* s_part = cst + 128;  // [4] wave sums
-  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nbig = o.info[kInfoBig], nhuge = o.info[kInfoHuge];
   if (B.flags & (kFlagPayloadOnly | kFlagNoCrc)) return;
-  if (blockIdx.x * kWavesPerBlock >= nbig && blockIdx.x >= nhuge) return;  // workgroup-uniform
-  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) tab[i] = crc_tab[i];  // slice-by-4 + x^8192
-  for (uint32_t i = threadIdx.x; i < 1024u; i += kWaveBlock) A4[i] = crc_tab[4096 + i];
-  for (uint32_t i = threadIdx.x; i < 128u; i += kWaveBlock) cst[i] = consts[i];
+  const uint64_t ctr = *reinterpret_cast<const uint64_t*>(o.info + kInfoCrcCtr);
+  const uint32_t nrec = (uint32_t)(ctr >> kCrcIdxShift);
+  const uint64_t TR = ctr & kCrcRoundMask;
+  if (!nrec) return;  // (grid-uniform)
+  uint32_t* tab = lds;         // [16][256] slice-by-16
+  uint32_t* A1 = lds + 4096;   // [4][256] (x) x^8192
+  uint32_t* cst = lds + 5120;  // [kNumCst]
+  for (uint32_t i = threadIdx.x; i < 4096u; i += kLaneBlock) tab[i] = crc_tab[4096 + i];
+  for (uint32_t i = threadIdx.x; i < 1024u; i += kLaneBlock) A1[i] = crc_tab[1024 + i];
+  for (uint32_t i = threadIdx.x; i < kNumCst; i += kLaneBlock) cst[i] = consts[i];
   __syncthreads();
   const LdsTab<1> T{tab, 0};
-  // records within the wave stage size: one wave each
-  for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nbig; i += gridDim.x * kWavesPerBlock) {
-    const uint32_t r = o.big_list[i];
-    const RecView v = rec_view(B, r);
-    const uint32_t pend = __builtin_amdgcn_readfirstlane((uint32_t)o.verdict[r]) & kVerdictPending;
-    if (v.e - v.st < 16 || pend) continue;  // (wave-uniform) role 1's record
-    const uint64_t a = v.p0, b = v.e - 4;
-    const uint32_t c = b - a >= 64 ? crc_one_wave(B.bytes, a, b, T, A1, cst, lane) : crc_serial<1>(B.bytes, a, b, T);
-    const bool good = crc_mask(c) == load_u32_unaligned(B.bytes, b);
-    if (lane == 0 && good) set_data_crc(B, o, r);
-    if (!good && (B.flags & kFlagStrictCrc)) strict_reject(o, B.n, n_slots, r, o.verdict[r], lane, 64);
+  const bool tab_at0 = (uint32_t)(uintptr_t)tab == 0u;  // (the asm chunk path addresses LDS 0)
+  const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
+  const uint64_t W = (uint64_t)gridDim.x * (kLaneBlock / 64), wv = (uint64_t)blockIdx.x * (kLaneBlock / 64) + wib;
+  const uint64_t R0 = TR * wv / W, R1 = TR * (wv + 1) / W;
+  if (R0 >= R1) return;  // (wave-uniform; no barrier follows)
+  PHASE_MARK(q0);
+  // the list entry holding flat round R0: 64-ary search over the ascending bases
+  uint32_t lo = 0, hi = nrec;  // base[lo] <= R0 < base[hi] (base[nrec] = TR)
+  while (hi - lo > 1u) {
+    const uint32_t step = (hi - lo + 63u) >> 6;
+    const uint32_t k = lo + lane * step;
+    const uint64_t bk = k < hi ? o.crc_base[k] : ~0ull;
+    lo = rfl32(lo + ((uint32_t)__popcll(__ballot(bk <= R0)) - 1u) * step);
+    hi = rfl32(lo + step < hi ? lo + step : hi);
   }
-  // larger records: one workgroup each
-  for (uint32_t i = blockIdx.x; i < nhuge; i += gridDim.x) {  // workgroup-uniform
-    PHASE_MARK(h0);
-    const uint32_t r = o.big_list[B.n - 1u - i];
-    const RecView v = rec_view(B, r);
-    // no payload CRC (lane_max below the framing size), or role 1's record (workgroup-uniform: a
-    // thread may read role 1's final verdict while another still reads the marker)
-    const int pend = __syncthreads_or((o.verdict[r] & kVerdictPending) != 0);
-    if (v.e - v.st < 16 || pend) continue;
-    const uint64_t a = v.p0, b = v.e - 4;
-    uint32_t c;
-    if (b - a >= 64) {
-      uint32_t t = crc_huge_wave(B.bytes, a, b, T, A4, cst, wib, lane);
-      if (wib) t = gf_mul(t, cst[80 + wib]);
-      if (lane == 0) s_part[wib] = t;
-      __syncthreads();
-      const uint64_t c1 = (b - 1) >> 4;
-      const uint32_t z = (uint32_t)(16ull * (c1 + 1ull) - b);  // zero bytes padding the last chunk
-      c = ~gf_mul(s_part[0] ^ s_part[1] ^ s_part[2] ^ s_part[3], cst[64 + z]);
-      __syncthreads();  // s_part is rewritten by the next record
-    } else {
-      c = crc_serial<1>(B.bytes, a, b, T);
+  uint32_t win0 = lo;
+  CrcWin w = crc_win_load(B, o, win0, nrec, TR, lane);
+  uint64_t lim = rl64(w.base, 63);
+  lim = lim < R1 ? lim : R1;
+  PHASE_MARK(q1);
+  PHASE_ADD(21, q0, q1);
+  int cur = -1;  // window entry of the open slice
+  uint64_t Rf = 0;
+  uint32_t S = 0;
+  // Groups of kCrcDepth rounds, double-buffered: the loads of group k+1 are in flight while group k
+  // is summed (a group never crosses the window; the pipeline drains at a window change).
+  struct Grp {
+    uint4 wd[kCrcDepth];
+    uint64_t rd[kCrcDepth];  // (scalar) flat round of load d
+    uint32_t kd[kCrcDepth];  // (scalar) its window entry
+    uint32_t n;              // rounds in the group (0: none before the window bound)
+    uint64_t r0;
+  };
+  auto issue = [&](Grp& g, uint64_t Rs) {
+    g.r0 = Rs;
+    g.n = Rs < lim ? (uint32_t)(lim - Rs < (uint64_t)kCrcDepth ? lim - Rs : (uint64_t)kCrcDepth) : 0u;
+    if (!g.n) return;
+#pragma unroll
+    for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
+      g.rd[d] = Rs + ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u);
+      g.kd[d] = (uint32_t)__popcll(__ballot(w.base <= g.rd[d])) - 1u;
+      const uint64_t c0 = rl64(w.c0, g.kd[d]);
+      const uint64_t ch = rl64(w.E, g.kd[d]) + 64ull * g.rd[d] - lane;
+      g.wd[d] = *reinterpret_cast<const uint4*>(B.bytes + (((int64_t)ch >= (int64_t)c0 ? ch : c0) << 4));
     }
-    const bool good = crc_mask(c) == load_u32_unaligned(B.bytes, b);
-    if (threadIdx.x == 0 && good) set_data_crc(B, o, r);
-    if (!good && (B.flags & kFlagStrictCrc) && threadIdx.x < 64)
-      strict_reject(o, B.n, n_slots, r, o.verdict[r], threadIdx.x, 64);
-    PHASE_MARK(h1);
-    if (threadIdx.x == 0) PHASE_ADD(13, h0, h1);
+  };
+  auto process = [&](const Grp& g) {
+    // chunk sums of the whole group, unconditionally (a conditional use lets the compiler sink each
+    // load to it: one round trip per round); only a record's first and last rounds (scalar test)
+    // take the masked path
+    uint32_t rc[kCrcDepth];
+    bool edge = false;  // (scalar) a record's first or last round in the group
+#pragma unroll
+    for (int d = 0; d < kCrcDepth; ++d) {
+      const uint64_t bas = rl64(w.base, g.kd[d]);
+      edge |= g.rd[d] == bas || g.rd[d] == bas + rl32(w.J, g.kd[d]) - 1u;
+    }
+    if (!edge && tab_at0) {  // interior group: one LDS round trip per chunk
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_u16_lds0(g.wd[d]);
+    } else if (!edge) {
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);
+    } else {
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) {
+        const uint64_t bas = rl64(w.base, g.kd[d]);
+        const uint32_t J = rl32(w.J, g.kd[d]);
+        if (g.rd[d] == bas || g.rd[d] == bas + J - 1u) {
+          const uint64_t ch = rl64(w.E, g.kd[d]) + 64ull * g.rd[d] - lane;
+          const uint64_t a = rl64(w.a, g.kd[d]), b = rl64(w.b, g.kd[d]);
+          rc[d] = (int64_t)ch >= (int64_t)rl64(w.c0, g.kd[d]) ? chunk_u(g.wd[d], ch << 4, a, b, T) : 0u;
+        } else {
+          rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);  // (interior: no masks)
+        }
+      }
+    }
+    // the group one record at a time: a record change ends the pass at `stop` (one flush site)
+    for (uint32_t d0 = 0;;) {
+      uint32_t stop = g.n;
+      int next = cur;
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) {
+        if ((uint32_t)d < d0 || (uint32_t)d >= stop) continue;  // (wave-uniform)
+        if ((int)g.kd[d] != cur) {
+          stop = (uint32_t)d;
+          next = (int)g.kd[d];
+          continue;
+        }
+        S = mul_tab(A1, S) ^ rc[d];
+      }
+      if (stop == g.n) break;
+      if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
+      cur = next;
+      Rf = g.r0 + stop;
+      S = 0;
+      d0 = stop;
+    }
+  };
+  uint64_t R = R0;
+  while (R < R1) {
+    if (R >= lim) {  // next window (R is its first entry's first round)
+      if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
+      cur = -1;
+      win0 += 63u;
+      w = crc_win_load(B, o, win0, nrec, TR, lane);
+      lim = rl64(w.base, 63);
+      lim = lim < R1 ? lim : R1;
+      continue;
+    }
+    Grp ga, gb;
+    issue(ga, R);
+    R += ga.n;
+    for (;;) {
+      issue(gb, R);
+      R += gb.n;
+      process(ga);
+      if (!gb.n) break;
+      issue(ga, R);
+      R += ga.n;
+      process(gb);
+      if (!ga.n) break;
+    }
   }
+  if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
+  PHASE_MARK(q9);
+  PHASE_ADD(25, q0, q9);
 }
 
-// The exception paths before the row-split scan in ONE launch (usually both empty): the exact walker
-// for the slow list (role 1), then the payload CRC of records above lane_max (role 2). Strict CRC
-// mode launches them separately (roles 1, then 2), because a strict rejection in role 2 reads the
-// status role 1 wrote for the same record.
+// The exact walker for the slow list before the row-split scan (usually empty: a workgroup leaves at
+// once when it has nothing to do).
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab,
-                                                           const uint32_t* __restrict__ consts, uint32_t lane_max,
-                                                           uint32_t roles) {
-  if (roles & 1u) role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
-  if (roles == 3u) __syncthreads();  // the LDS tables are reloaded by role 2
-  if (roles & 2u) role_big_crc(B, o, crc_tab, consts, sc.n_slots);
+                                                           const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
+  role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
+}
+
+// The streaming payload CRC of the large records, after the slow walker (a strict rejection reads
+// the status it wrote) and before the scan (a rejection withdraws counts). Its own launch: the slow
+// walker's registers would cost it a third of its resident waves.
+__global__ __launch_bounds__(kLaneBlock, TFRG_CRC_WAVES) void k_crc_stream(DevBatch B, DevOut o,
+                                                                          const uint32_t* __restrict__ crc_tab,
+                                                                          const uint32_t* __restrict__ consts,
+                                                                          uint32_t n_slots) {
+  role_crc_stream(B, o, crc_tab, consts, n_slots);
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in
@@ -1885,15 +2100,6 @@ __device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t
 constexpr int kSpineBlock = 256;
 constexpr int kSpineItems = 16;
 static_assert(kSpineBlock * kSpineItems == (1 << kSpineChunkShift), "one chunk per spine workgroup");
-
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += y;
-  }
-  return v;
-}
 
 // exclusive prefix of chunk `chunk` from its predecessors' look-back words (lb[0..chunk))
 __device__ __forceinline__ uint32_t spine_look_back(const uint64_t* lb, uint32_t chunk) {
@@ -2569,7 +2775,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_spine",
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_crc_stream", "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2593,12 +2799,12 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
 
   mark(kStageLaneCount);
   // one round of resident workgroups (a second, partial round would idle most CUs at the tail)
-  auto resident_grid = [&](const void* fn, size_t lds) {
+  auto resident_grid = [&](const void* fn, size_t lds, bool cap = true) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLaneBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus;
-    return g < cfg.lane_grid ? g : cfg.lane_grid;
+    return g < cfg.lane_grid || !cap ? g : cfg.lane_grid;
   };
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
@@ -2616,22 +2822,24 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageTailCount);
-  // the exception paths before the scan (slow records, payload CRCs of large records) are usually
-  // empty: one launch, grid-stride loops, a workgroup leaves at once when it has nothing to do
+  // the exact walker for the slow list (usually empty): grid-stride, a workgroup leaves at once when
+  // it has nothing to do
   {
     const bool gord = slow_lds > kLaneLdsBudget;
-    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_lds, (3072 + 128 + 4) * 4);
+    const size_t lds = gord ? 2048ull * 4 : slow_lds;
     const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
-    const bool strict = (b.flags & kFlagStrictCrc) != 0;
-    for (uint32_t roles : {strict ? 1u : 3u, strict ? 2u : 0u}) {
-      if (!roles) continue;
-      if (gord)
-        hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab, d_consts,
-                           cfg.lane_max, roles);
-      else
-        hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
-                           d_consts, cfg.lane_max, roles);
-    }
+    if (gord)
+      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
+                         cfg.lane_max);
+    else
+      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
+                         cfg.lane_max);
+  }
+  mark(kStageCrc);
+  {  // one round of resident workgroups: the large payloads split evenly over the waves
+    const size_t lds = (5120 + kNumCst) * 4;
+    const uint32_t g = (uint32_t)resident_grid(reinterpret_cast<const void*>(&k_crc_stream), lds, false);
+    hipLaunchKernelGGL(k_crc_stream, dim3(g), dim3(kLaneBlock), lds, st, b, o, d_tab, d_consts, (uint32_t)S);
   }
   mark(kStageSpine);
   if (S > 0)

@@ -69,7 +69,8 @@ def main():
         L.tfrg_debug_phase(arr, 32, 1)
         names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
                  "c.bails", "g.stage+meta", "g.groups", "g.int64", "g.lane", "h.crc", "h.walk", "g.float",
-                 "l.span+stage", "l.crc", "l.walk", "l.final", "l.total"]
+                 "l.span+stage", "l.crc", "l.walk", "l.final", "l.total", "s.search", "s.load+chunk",
+                 "s.horner+flush", "-", "s.total", "s.batches"]
         tot = (arr[20] or arr[7]) or 1
         for i, nm in enumerate(names):
             print(f"{nm:10s} {arr[i]:>16d} {arr[i] / tot:8.3f}")
