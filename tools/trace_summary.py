@@ -1,11 +1,8 @@
 #!/usr/bin/env python3
-"""Per-kernel durations of the FULL-batch dispatches in a rocprofv3 kernel trace.
+"""Per-(kernel, grid) duration summary of a rocprofv3 --kernel-trace CSV (bench.py runs several
+workloads and sample batches in one process: grouping by grid separates the full batches).
 
-usage: trace_summary.py <run_kernel_trace.csv>
-bench.py also decodes a small sample batch (schema discovery) and the profile run times a
-streaming-read probe; rocprofv3's --stats averages mix those in. This keeps, per kernel name,
-the dispatches with that kernel's largest grid (the timed batch) and prints count / mean / min /
-max in microseconds — the numbers comparable with bench.py's kernels_ms.
+usage: trace_summary.py <run_kernel_trace.csv> [min_calls]
 """
 import csv
 import sys
@@ -13,20 +10,19 @@ from collections import defaultdict
 
 
 def main() -> None:
-    rows = list(csv.DictReader(open(sys.argv[1])))
-    by = defaultdict(list)
-    for r in rows:
+    path = sys.argv[1]
+    min_calls = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    groups = defaultdict(list)
+    for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
-        by[name].append((grid, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3))
-    out = []
-    for name, v in by.items():
-        g = max(x[0] for x in v)
-        d = [t for gr, t in v if gr == g]
-        out.append((sum(d) / len(d), name, len(d), min(d), max(d), g))
-    print(f"{'kernel':58s} {'n':>4s} {'mean_us':>10s} {'min_us':>10s} {'max_us':>10s} {'grid':>10s}")
-    for mean, name, n, lo, hi, g in sorted(out, reverse=True):
-        print(f"{name[:58]:58s} {n:4d} {mean:10.1f} {lo:10.1f} {hi:10.1f} {g:10d}")
+        grid = r.get("Grid_Size_X") or r.get("Grid_Size")
+        groups[(name, int(grid))].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    print(f"{'kernel':44s} {'grid':>9s} {'calls':>6s} {'mean_us':>10s} {'median_us':>10s} {'min_us':>9s} {'max_us':>9s}")
+    for (name, grid), d in sorted(groups.items(), key=lambda kv: -sum(kv[1])):
+        if len(d) < min_calls:
+            continue
+        d.sort()
+        print(f"{name:44s} {grid:9d} {len(d):6d} {sum(d) / len(d):10.1f} {d[len(d) // 2]:10.1f} {d[0]:9.1f} {d[-1]:9.1f}")
 
 
 if __name__ == "__main__":
