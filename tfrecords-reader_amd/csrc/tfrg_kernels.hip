@@ -748,7 +748,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-constexpr uint32_t kWStage = 12288;                 // staged record bytes per wave (wavefront kernels)
+#ifndef TFRG_WSTAGE
+#define TFRG_WSTAGE 12288
+#endif
+constexpr uint32_t kWStage = TFRG_WSTAGE;           // staged record bytes per wave (wavefront kernels)
 constexpr uint32_t kWStageStride = kWStage + 64;
 
 // copy absolute bytes [lo16, hi) (lo16 16-aligned, wave-uniform, hi - lo16 <= kStageBytes) into dst
@@ -874,6 +877,8 @@ struct FastSrc {
   // 4 bytes at payload offset i, unmasked (the canonical walker bounds-checks what it uses)
   __device__ __forceinline__ uint32_t u32(uint32_t i) const { return lds_u32u(l, p + i); }
   __device__ __forceinline__ void window(uint32_t) const {}  // (the stage is the window)
+  __device__ __forceinline__ void prefetch(uint32_t) const {}
+  __device__ __forceinline__ void advance() const {}
 };
 
 // The same payload view over HBM (records beyond the LDS stage): two aligned dword loads + a byte
@@ -891,6 +896,9 @@ struct FastSrcG {
   mutable uint64_t wa = 0;  // window start (16-aligned absolute address)
   mutable bool wv = false;  // window loaded
   mutable uint4 b0, b1;
+  mutable uint64_t pa = ~0ull;  // prefetched window of the next map entry (its start, validity, blocks)
+  mutable bool pv = false;
+  mutable uint4 p0, p1;
   __device__ __forceinline__ void window(uint32_t i) const {
     if (!WIN) return;
     const uint64_t a = (base + i) & ~15ull;
@@ -899,6 +907,25 @@ struct FastSrcG {
     wa = a;
     b0 = *reinterpret_cast<const uint4*>(buf + (a < lb ? a : lb));
     b1 = *reinterpret_cast<const uint4*>(buf + (a + 16u < lb ? a + 16u : lb));
+  }
+  // the next entry's window, requested as soon as this entry's extent is known (it then overlaps
+  // this entry's key lookup and list-count loads instead of adding a round trip per entry), made the
+  // window by advance() at the end of the entry (plain register moves, no condition)
+  __device__ __forceinline__ void advance() const {
+    if (!WIN) return;
+    wa = pa;
+    wv = pv;
+    b0 = p0;
+    b1 = p1;
+  }
+  __device__ __forceinline__ void prefetch(uint32_t i) const {
+    if (!WIN) return;
+    const uint64_t a = (base + i) & ~15ull;
+    pv = a + 32u <= lim + 4u;
+    const uint64_t lb = lim - 12u;
+    pa = a;
+    p0 = *reinterpret_cast<const uint4*>(buf + (a < lb ? a : lb));
+    p1 = *reinterpret_cast<const uint4*>(buf + (a + 16u < lb ? a + 16u : lb));
   }
   __device__ __forceinline__ uint32_t u32(uint32_t i) const {
     const uint64_t a = base + i;
@@ -1212,12 +1239,13 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
   uint64_t seen = 0;  // key ids < 64 already in the dict (a duplicate key bails)
   uint32_t rank = 0;
   const uint32_t fe = fo + fl;
+  if (ok && fo < fe) s.window(fo);  // (later entries' windows are prefetched)
   for (uint32_t q = fo; ok && q < fe;) {
     uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
-    s.window(q);
     ok = hdr2(s, q, fe, en, eo, el) & (en == 1u);
     const uint32_t ee = eo + el;
     q = ee;
+    s.prefetch(q);
     ok &= hdr2(s, eo, ee, kn, ko, kl) & (kn == 1u);
     ok &= hdr2(s, ko + kl, ee, vn, vo, vl) & (vn == 2u) & (vo + vl == ee);
     ok &= hdr2(s, vo, ee, kind, lo, ll) & (lo + ll == ee) & (kind - 1u < 3u);
@@ -1283,6 +1311,7 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
       }
     }
     sink.fast_put((uint32_t)slot, rank, cw, lv);
+    s.advance();
   }
   sink.rank = rank;
   return ok ? TFRG_OK : kBail;
@@ -1943,14 +1972,16 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   };
   auto process = [&](const Grp& g) {
     // chunk sums of the whole group, unconditionally (a conditional use lets the compiler sink each
-    // load to it: one round trip per round); only a record's first and last rounds (scalar test)
-    // take the masked path
+    // load to it: one round trip per round); only the edge rounds (scalar test) take the masked path
     uint32_t rc[kCrcDepth];
-    bool edge = false;  // (scalar) a record's first or last round in the group
+    // (scalar) a round that needs masks in the group: a record's first two rounds (its first 4 payload
+    // bytes, inverted, may run into the chunk after a's: that chunk opens the second round when the
+    // first holds only a's chunk) and its last round
+    bool edge = false;
 #pragma unroll
     for (int d = 0; d < kCrcDepth; ++d) {
       const uint64_t bas = rl64(w.base, g.kd[d]);
-      edge |= g.rd[d] == bas || g.rd[d] == bas + rl32(w.J, g.kd[d]) - 1u;
+      edge |= g.rd[d] <= bas + 1u || g.rd[d] == bas + rl32(w.J, g.kd[d]) - 1u;
     }
     if (!edge && tab_at0) {  // interior group: one LDS round trip per chunk
 #pragma unroll
@@ -1963,7 +1994,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
       for (int d = 0; d < kCrcDepth; ++d) {
         const uint64_t bas = rl64(w.base, g.kd[d]);
         const uint32_t J = rl32(w.J, g.kd[d]);
-        if (g.rd[d] == bas || g.rd[d] == bas + J - 1u) {
+        if (g.rd[d] <= bas + 1u || g.rd[d] == bas + J - 1u) {
           const uint64_t ch = rl64(w.E, g.kd[d]) + 64ull * g.rd[d] - lane;
           const uint64_t a = rl64(w.a, g.kd[d]), b = rl64(w.b, g.kd[d]);
           rc[d] = (int64_t)ch >= (int64_t)rl64(w.c0, g.kd[d]) ? chunk_u(g.wd[d], ch << 4, a, b, T) : 0u;
@@ -2074,7 +2105,7 @@ struct Pref {  // named fields, returned by value: an array or an out-parameter 
 
 __device__ __forceinline__ Pref pref_load_v(const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
   Pref p;
-  static_assert(kPrefWords == 12, "pref_load is spelled out for 12 words");
+  static_assert(kPrefWords <= 12 && kWStage % 1024 == 0, "pref_load is spelled out for up to 12 words");
   TFRG_PREF_LOAD(0) TFRG_PREF_LOAD(1) TFRG_PREF_LOAD(2) TFRG_PREF_LOAD(3) TFRG_PREF_LOAD(4) TFRG_PREF_LOAD(5)
   TFRG_PREF_LOAD(6) TFRG_PREF_LOAD(7) TFRG_PREF_LOAD(8) TFRG_PREF_LOAD(9) TFRG_PREF_LOAD(10) TFRG_PREF_LOAD(11)
   return p;
@@ -2678,7 +2709,14 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   PHASE_ADD(12, g1, g2);
 }
 
-// Medium records: staged in LDS with the same register pipeline as k_stage_count.
+// Medium records, one wave each, staged in LDS. TFRG_GATHER_PREF = 1 (default) loads the next
+// record's bytes into registers while this one is gathered (48 VGPRs live across the gather);
+// 0 stages each record when it starts: 4 instead of 3 waves' registers per SIMD, but the 12 KiB
+// stages cap the CU at 12 waves anyway (C3 gather 1.654 vs 1.636 ms; a 9 KiB stage for 16 waves
+// sent C3's larger records to the HBM path: 1.918 ms).
+#ifndef TFRG_GATHER_PREF
+#define TFRG_GATHER_PREF 1
+#endif
 template <bool COMPAT>
 __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -2691,7 +2729,9 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
   q.s1 = B.start[q.r1];
   q.e1 = B.end[q.r1];
   q.t1 = i < nbig ? o.status[q.r1] : -1;
+#if TFRG_GATHER_PREF
   Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
+#endif
   q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
   q.s2v = B.start[vgpr_launder(q.r2)];
   q.e2v = B.end[vgpr_launder(q.r2)];
@@ -2703,7 +2743,14 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     const bool ok = q.t1 == TFRG_OK;
     const RecView v = rec_view_se(B, q.s1, q.e1);
     const uint64_t lo16 = v.st & ~15ull;
+#if TFRG_GATHER_PREF
     if (ok) pref_store(pf, stage, lo16, v.e, lane);
+#else
+    if (ok) {  // this record's bytes: all loads in flight, then the stores (registers live only here)
+      const Pref cur = pref_load_v(B.bytes, lo16, v.e, lane);
+      pref_store(cur, stage, lo16, v.e, lane);
+    }
+#endif
     wave_lds_sync();
     // slot metadata of this record (issued ahead of the next record's byte loads)
     bool present = false;
@@ -2724,7 +2771,9 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     q.t1 = i + stride < nbig ? (int32_t)rfl32((uint32_t)q.t2v) : -1;
     q.r2 = rfl32(q.r3v);
     q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
+#if TFRG_GATHER_PREF
     pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
+#endif
     q.s2v = B.start[vgpr_launder(q.r2)];
     q.e2v = B.end[vgpr_launder(q.r2)];
     q.t2v = o.status[vgpr_launder(q.r2)];
