@@ -101,6 +101,18 @@ int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
  * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
 int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
 
+/* Record-shape templates (no reference counterpart: a fast path under decoder.pyx:107-300). Up to 4
+ * shapes of canonical records (payload <= 256 bytes) -- every byte fixed except list contents, incl.
+ * the continuation bits of packed int64 lists -- are learned from up to 4,096 host records; a record
+ * equal to a template under its mask gets the template's dict without the canonical walk (its
+ * values are still read from the record). Learned automatically from the first tfrg_decode_host
+ * batch after each tfrg_set_schema; device-only callers pass a host sample here. Returns the number
+ * of templates (0..4). tfrg_ctx_set_templates(ctx, 0) disables them (env TFRG_TEMPLATES=0). */
+int tfrg_learn_templates(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                         const uint64_t* h_end, uint32_t n, uint32_t flags);
+int tfrg_template_count(tfrg_ctx* ctx);
+int tfrg_ctx_set_templates(tfrg_ctx* ctx, int on);
+
 /* Per-kernel timing: with profiling on, every decode records HIP events on its stream around
  * each kernel stage; tfrg_profile_last waits for the last decode and writes up to cap stage
  * durations (ms) and names, returning the stage count. */

@@ -1,9 +1,13 @@
 // tfrg_capi.cpp — device context of libtfrg: key table upload, HBM arena, decode orchestration and
 // result transfer (include/tfrg.h). The kernels live in tfrg_kernels.hip.
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
+#include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/tfrg.h"
@@ -84,6 +88,13 @@ struct tfrg_ctx {
   uint64_t nbytes = 0;
   uint64_t cap_i64 = 0, cap_f32 = 0, cap_b = 0;
   bool have_result = false;
+  // record-shape templates (tfrg_learn_templates): host key table, device templates
+  std::unordered_map<std::string, uint32_t> key_id;
+  std::vector<int32_t> key_slot_h;  // [4 * key]: flags, slot per kind
+  DBuf tpl;
+  uint32_t n_tpl = 0;
+  bool tpl_learned = false;
+  bool tpl_on = true;
   // optional per-stage HIP events (tfrg_ctx_set_profiling)
   bool profiling = false;
   bool have_events = false;
@@ -103,6 +114,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   HIP_TRY(hipSetDevice(device));
   tfrg_ctx* c = new tfrg_ctx();
   c->device = device;
+  if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -144,7 +156,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
-                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part};
+                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl};
   for (DBuf* b : all) b->release();
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
@@ -261,6 +273,12 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   c->n_keys = n_keys;
   c->n_slots = n_slots;
   c->ht_mask = hsz - 1;
+  c->key_id.clear();
+  for (uint32_t k = 0; k < n_keys; ++k)
+    c->key_id.emplace(std::string((const char*)key_blob + key_offsets[k], key_offsets[k + 1] - key_offsets[k]), k);
+  c->key_slot_h = ks;
+  c->n_tpl = 0;  // slots may have moved: learn again from the next host batch
+  c->tpl_learned = false;
   return 0;
 }
 
@@ -277,7 +295,184 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.slot_kind = c->slot_kind.as<uint8_t>();
   s.key_w = c->key_w.as<uint32_t>();
   s.krec = c->krec.as<uint32_t>();
+  s.tpl = c->tpl.as<uint32_t>();
+  s.n_tpl = c->tpl_on ? c->n_tpl : 0u;
   return s;
+}
+
+// ---- record-shape templates (tfrg_internal.h): learned from host records --------------------------
+namespace {
+
+// k_lane_count's hdr2 (tfrg_kernels.hip): 1-byte tag of wire type 2, 1..3-byte length, body in end
+bool tpl_hdr2(const uint8_t* p, uint32_t L, uint32_t pos, uint32_t end, uint32_t& fn, uint32_t& off, uint32_t& len) {
+  if (pos >= L || (p[pos] & 0x87u) != 0x02u) return false;
+  fn = (p[pos] >> 3) & 0xfu;
+  uint32_t q = pos + 1, l = 0;
+  for (uint32_t nb = 0;; ++nb) {
+    if (nb == 3 || q >= L) return false;
+    const uint32_t b = p[q++];
+    l |= (b & 0x7fu) << (7 * nb);
+    if (!(b & 0x80u)) break;
+  }
+  off = q;
+  len = l;
+  return off <= end && l <= end - off;
+}
+
+struct Tpl {
+  uint32_t L = 0;
+  std::vector<uint8_t> bytes, mask;
+  std::vector<uint32_t> ent;  // 4 words per entry
+  std::string key() const {  // identity: length, masked bytes, mask
+    std::string k((const char*)&L, 4);
+    for (uint32_t i = 0; i < L; ++i) k.push_back((char)(bytes[i] & mask[i]));
+    k.append((const char*)mask.data(), mask.size());
+    return k;
+  }
+};
+
+// The dict fast_walk (tfrg_kernels.hip) builds for this payload, as a template; false where
+// fast_walk would bail (or the shape does not fit a template).
+bool tpl_derive(const tfrg_ctx* c, const uint8_t* p, uint32_t L, Tpl& t) {
+  if (L < 2 || L > kTplMaxL) return false;
+  t.L = L;
+  t.bytes.assign(p, p + L);
+  t.mask.assign(L, 0xffu);
+  t.ent.clear();
+  uint32_t fn, fo, fl;
+  if (!tpl_hdr2(p, L, 0, L, fn, fo, fl) || fn != 1u || fo + fl != L) return false;
+  std::vector<uint32_t> seen;
+  uint32_t rank = 0;
+  for (uint32_t q = fo; q < L;) {
+    uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
+    if (!tpl_hdr2(p, L, q, L, en, eo, el) || en != 1u) return false;
+    const uint32_t ee = eo + el;
+    q = ee;
+    if (!tpl_hdr2(p, L, eo, ee, kn, ko, kl) || kn != 1u) return false;
+    if (!tpl_hdr2(p, L, ko + kl, ee, vn, vo, vl) || vn != 2u || vo + vl != ee) return false;
+    if (!tpl_hdr2(p, L, vo, ee, kind, lo, ll) || lo + ll != ee || kind < 1u || kind > 3u) return false;
+    if (kl > 256u) return false;
+    const auto it = c->key_id.find(std::string((const char*)p + ko, kl));
+    if (it == c->key_id.end()) return false;
+    const uint32_t kid = it->second;
+    if (c->key_slot_h[4ull * kid] & 1) return false;  // invalid UTF-8 key: the exact path
+    const int32_t slot = c->key_slot_h[4ull * kid + kind];
+    if (slot < 0 || std::find(seen.begin(), seen.end(), kid) != seen.end()) return false;
+    seen.push_back(kid);
+    uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0;
+    const uint32_t le = lo + ll;
+    for (uint32_t g = lo; g < le;) {
+      uint32_t cf, co, cl;
+      if (!tpl_hdr2(p, L, g, le, cf, co, cl) || cf != 1u) return false;
+      g = co + cl;
+      if (kind == TFRG_KIND_BYTES) {
+        ++cnt;
+        std::fill(t.mask.begin() + co, t.mask.begin() + co + cl, 0);
+      } else if (kind == TFRG_KIND_FLOAT) {
+        if (cl & 3u) return false;
+        cnt += cl >> 2;
+        std::fill(t.mask.begin() + co, t.mask.begin() + co + cl, 0);
+      } else {  // packed varints: terminated, none longer than 10 bytes; their boundaries are fixed
+        uint32_t run = 0;
+        for (uint32_t i = co; i < co + cl; ++i) {
+          t.mask[i] = 0x80u;
+          if (p[i] & 0x80u) {
+            if (++run >= 10u) return false;
+          } else {
+            run = 0;
+            ++cnt;
+          }
+        }
+        if (cl && (p[co + cl - 1] & 0x80u)) return false;
+      }
+      if (nch == 0) {
+        c0o = co;
+        c0l = cl;
+      }
+      ++nch;
+    }
+    if (rank >= 65534u || t.ent.size() / 4 >= kTplMaxEntries) return false;
+    ++rank;
+    uint32_t mode = 0, cw = cnt, a = lo, b = ll;
+    if (cnt == 1u && nch == 1u) {
+      if (kind == TFRG_KIND_BYTES) {
+        mode = 3;
+      } else if (kind == TFRG_KIND_FLOAT) {
+        mode = 2;
+      } else if (c0l <= 4u) {
+        mode = 1;
+      }
+      if (mode) {
+        cw = 1u | kCountInline;
+        a = c0o;
+        b = c0l;
+      }
+    }
+    t.ent.insert(t.ent.end(), {(uint32_t)slot | (mode << 24), rank, cw, a | (b << 16)});
+  }
+  return !t.ent.empty();
+}
+
+}  // namespace
+
+extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                                    const uint64_t* h_end, uint32_t n, uint32_t flags) {
+  if (!c || (n && (!h_bytes || !h_start || !h_end))) return TFRG_E_ARG;
+  c->tpl_learned = true;
+  c->n_tpl = 0;
+  if (!c->n_keys) return 0;
+  std::map<std::string, std::pair<uint32_t, Tpl>> seen;  // shape -> (records, template)
+  Tpl t;
+  const uint32_t lim = n < 4096u ? n : 4096u;
+  for (uint32_t i = 0; i < lim; ++i) {
+    uint64_t a = h_start[i], e = h_end[i];
+    if (e > nbytes || e < a) continue;
+    if (!(flags & TFRG_FLAG_PAYLOAD_ONLY)) {  // framed: a length field matching the range
+      if (e - a < 16) continue;
+      uint64_t len = 0;
+      memcpy(&len, h_bytes + a, 8);
+      if (len != e - a - 16) continue;
+      a += 12;
+      e -= 4;
+    }
+    if (!tpl_derive(c, h_bytes + a, (uint32_t)(e - a > 0xffffffffull ? 0 : e - a), t)) continue;
+    auto& slot = seen[t.key()];
+    if (!slot.first) slot.second = t;
+    ++slot.first;
+  }
+  std::vector<std::pair<uint32_t, const Tpl*>> order;
+  for (auto& kv : seen) order.push_back({kv.second.first, &kv.second.second});
+  std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMax);
+  if (!nt) return 0;
+  std::vector<uint32_t> w((size_t)nt * kTplWords, 0);
+  for (uint32_t k = 0; k < nt; ++k) {
+    const Tpl& x = *order[k].second;
+    uint32_t* d = &w[(size_t)k * kTplWords];
+    d[0] = x.L;
+    d[1] = (uint32_t)(x.ent.size() / 4);
+    d[2] = (x.L + 3) / 4;
+    memcpy(d + kTplBytes, x.bytes.data(), x.L);
+    memcpy(d + kTplMask, x.mask.data(), x.L);
+    memcpy(d + kTplEnt, x.ent.data(), x.ent.size() * 4);
+  }
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  if (c->tpl.ensure(w.size() * 4)) {
+    set_error("template allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(c->tpl.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  c->n_tpl = nt;
+  return (int)nt;
+}
+
+extern "C" int tfrg_template_count(tfrg_ctx* c) { return c ? (int)c->n_tpl : TFRG_E_ARG; }
+
+extern "C" int tfrg_ctx_set_templates(tfrg_ctx* c, int on) {
+  if (!c) return TFRG_E_ARG;
+  c->tpl_on = on != 0;
+  return 0;
 }
 
 int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_start,
@@ -478,6 +673,10 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
     if (b > a) total += b - a;
   }
   c->cap_hint = total;
+  if (!c->tpl_learned && c->n_keys && c->tpl_on) {  // record shapes of the first host batch of a schema
+    const int t = tfrg_learn_templates(c, h_bytes, nbytes, h_start, h_end, n, flags);
+    if (t < 0) return t;
+  }
   return tfrg_decode_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_start.as<uint64_t>(),
                             c->in_end.as<uint64_t>(), n, flags, st);
 }

@@ -20,7 +20,20 @@ struct DevSchema {
   const uint8_t* slot_kind;    // [n_slots]
   const uint32_t* key_w;       // [n_keys][2]: first / last 4 key bytes (see key_hash_words)
   const uint32_t* krec;        // [n_keys][8] packed key record, see KeyRec
+  const uint32_t* tpl;         // [n_tpl][kTplWords] record-shape templates (below), learned on the host
+  uint32_t n_tpl;
 };
+
+// Record-shape template: the payload of a canonical record whose every byte except list contents is
+// fixed (keys, tags, lengths, entry order; for packed int64 lists the continuation bits, i.e. the
+// varint boundaries). A record equal to it under the mask has exactly the template's dict (slots,
+// ranks, counts, list locations): the lane kernel then skips the canonical walk and reads only the
+// inline values. Layout (u32 words): [0] payload length L, [1] entries, [2] ceil(L/4), [3] 0,
+// [4, 4+64) bytes, [68, 68+64) mask, [132, 132+4*16) entries {slot | mode << 24, rank, count word,
+// a | b << 16}; mode 0: loc (a, b) = (list offset, list length), 1: inline int64 varint at a of b
+// bytes, 2: inline float at a, 3: inline bytes element at a of b bytes.
+constexpr uint32_t kTplMaxL = 256, kTplMaxEntries = 16, kTplMax = 4;
+constexpr uint32_t kTplBytes = 4, kTplMask = 68, kTplEnt = 132, kTplWords = 196;
 
 // Packed per-key record (8 x u32) staged into LDS by the lane kernels' fast path.
 enum KeyRec : uint32_t { kKrHash = 0, kKrLen, kKrW0, kKrW1, kKrSlot1, kKrSlot2, kKrSlot3, kKrFlags, kKrWords };

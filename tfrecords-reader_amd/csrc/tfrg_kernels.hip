@@ -1317,6 +1317,40 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
   return ok ? TFRG_OK : kBail;
 }
 
+// Record-shape templates (tfrg_internal.h, learned on the host): the first template this payload
+// equals under its mask, or -1 (wave-uniform loop over the templates, ~5 VALU per payload word).
+__device__ __forceinline__ int tpl_match(const FastSrc& fs, const uint32_t* tpl, uint32_t n_tpl) {
+  int hit = -1;
+  for (uint32_t t = 0; t < n_tpl; ++t) {
+    const uint32_t* T = tpl + t * kTplWords;
+    if (hit < 0 && fs.L == T[0]) {
+      const uint32_t nw = T[2];
+      uint32_t diff = 0;
+      for (uint32_t w = 0; w < nw; ++w) diff |= (fs.u32(4u * w) ^ T[kTplBytes + w]) & T[kTplMask + w];
+      if (!diff) hit = (int)t;
+    }
+  }
+  return hit;
+}
+
+// The matched template's dict, exactly as fast_walk builds it for this record: slots, ranks and
+// count words from the template, list locations or the inline values read from the record.
+template <class Sink>
+__device__ __forceinline__ void tpl_put(const FastSrc& fs, const uint32_t* T, Sink& sink) {
+  const uint32_t ne = T[1];
+  for (uint32_t e = 0; e < ne; ++e) {
+    const uint4 d = *reinterpret_cast<const uint4*>(T + kTplEnt + 4u * e);
+    const uint32_t mode = d.x >> 24, a = d.w & 0xffffu, b = d.w >> 16;
+    uint2 lv;
+    if (mode == 0u) lv = make_uint2(a, b);                                       // (list offset, length)
+    else if (mode == 1u) lv = make_uint2(vgroups(fs.u32(a), bytes_mask(b)), 0u);  // one int64 varint
+    else if (mode == 2u) lv = make_uint2(fs.u32(a), 0u);                          // one float
+    else lv = make_uint2((uint32_t)(fs.base + a), b);                             // one bytes element
+    sink.fast_put(d.x & 0xffffffu, d.y, d.z, lv);
+  }
+  sink.rank = ne;
+}
+
 // Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
 // bytes and of the payload (the TFRecord spec; absent from the reference), from the
 // wave's LDS stage (STAGED) or from HBM.
@@ -1446,6 +1480,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
+  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneBlock / 64) * 64u : 0u);  // templates
   for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
   if constexpr (MODE == 1) {
     tsl[lane] = 0;
@@ -1454,6 +1489,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneBlock) tpl_l[i] = sc.tpl[i];
   }
   __syncthreads();
   const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
@@ -1526,7 +1562,13 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       sink.fast_reset(S);
       if (strict_pass(B, v.verdict, true)) {  // (strict mode: a CRC failure is the slow kernel's)
         const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-        done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+        const int tm = sc.n_tpl ? tpl_match(fs, tpl_l, sc.n_tpl) : -1;
+        if (tm >= 0) {  // a known record shape: its dict without the walk
+          tpl_put(fs, tpl_l + (uint32_t)tm * kTplWords, sink);
+          done = true;
+        } else {
+          done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+        }
         tried = true;
       }
       PHASE_MARK(p3);
@@ -2840,9 +2882,10 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t dict_lane = S * kLaneBlock * 4 + r16(S * kLaneBlock * 2);  // cnt u32 + ord u16 per lane
   const size_t tab_lds = 256ull * kLaneSlice * kLaneRep * 4;
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
-  const size_t keys_lds = (sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt)
-                              ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
-  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds;
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
+  const size_t keys_lds = fast_ok ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
+  const size_t tpl_lds = fast_ok ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (after the MODE 1 tile sums)
+  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + tpl_lds;
   const size_t slow_lds = 2048ull * 4 + dict_lane;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
 
@@ -2860,12 +2903,12 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
                        dim3(kLaneBlock), lane_lds - tab_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else if (S <= 64) {
-    const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4;  // (+ the static tables)
+    const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   } else {
-    const size_t lds = stage_lds + keys_lds;  // (+ the static tables)
+    const size_t lds = stage_lds + keys_lds + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);

@@ -76,6 +76,10 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tfrg_ctx_set_lane_max": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_wave_stage": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "tfrg_learn_templates": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                                       C.c_uint32]),
+    "tfrg_template_count": (C.c_int, [C.c_void_p]),
+    "tfrg_ctx_set_templates": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
     "tfrg_stream_create": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
     "tfrg_stream_destroy": (C.c_int, [C.c_void_p]),

@@ -111,6 +111,23 @@ class HipDecoder:
     def set_lane_max(self, nbytes: int) -> None:
         N.check(self._lib.tfrg_ctx_set_lane_max(self._ctx, nbytes), "tfrg_ctx_set_lane_max")
 
+    def set_templates(self, on: bool) -> None:
+        """Record-shape templates (tfrg_learn_templates): on by default."""
+        N.check(self._lib.tfrg_ctx_set_templates(self._ctx, int(bool(on))), "tfrg_ctx_set_templates")
+
+    def template_count(self) -> int:
+        return int(self._lib.tfrg_template_count(self._ctx))
+
+    def learn_templates(self, buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, payload_only: bool = False) -> int:
+        """Learn record shapes from a host sample (device-only callers; tfrg_decode_host does it itself)."""
+        b = np.ascontiguousarray(buf, np.uint8)
+        st = np.ascontiguousarray(starts, np.uint64)
+        en = np.ascontiguousarray(ends, np.uint64)
+        k = self._lib.tfrg_learn_templates(self._ctx, N.ptr(b), b.size, N.ptr(st), N.ptr(en), st.size,
+                                           N.FLAG_PAYLOAD_ONLY if payload_only else 0)
+        N.check(min(k, 0), "tfrg_learn_templates")
+        return int(k)
+
     def set_wave_stage(self, nbytes: int) -> None:
         """Records above lane_max spanning <= nbytes go to the LDS-staged wavefront kernels."""
         N.check(self._lib.tfrg_ctx_set_wave_stage(self._ctx, nbytes), "tfrg_ctx_set_wave_stage")
