@@ -212,3 +212,40 @@ def test_long_varint_mid_list_above_lane_max(dec, orc):
         if ost == 0:
             assert G.canon_entries(raw_entries(r, i)) == G.canon_entries(ent)
     assert int(r.status[1]) == S.ERR_VARINT_TOO_MANY
+
+
+def test_load_ranges_bounds_slots_times_records(orc, tmp_path, monkeypatch):
+    """A sparse key set (every record its own key): load_ranges splits the batch by records so that
+    slots x records stays under SLOT_BUDGET_BYTES; values and order are those of one batch."""
+    from tfr_reader import indexer, reader, writer
+
+    pl = [example(entry(f"k{i}".encode(), i64(i)), entry(b"shared", f32(float(i)))) for i in range(3000)]
+    p = tmp_path / "sparse.tfrecord"
+    writer.write_tfrecord(p, pl)
+    ptrs = indexer.native.index_buffer(p.read_bytes())
+    calls = []
+    real = reader._decode_bounded
+
+    def spy(dec, buf, st, en):
+        for at, res in real(dec, buf, st, en):
+            calls.append((at, int(res.status.size)))
+            yield at, res
+
+    monkeypatch.setattr(reader, "SLOT_BUDGET_BYTES", 18 * 1024 * 64)  # 1,024 records at 64 slots
+    monkeypatch.setattr(reader, "_decode_bounded", spy)
+    order = np.random.default_rng(0).permutation(3000)
+    reader.load_ranges([str(p)] * 3000, ptrs[:, 0], ptrs[:, 1])  # (learns the 3,001 keys)
+    calls.clear()
+    feats = reader.load_ranges([str(p)] * 3000, ptrs[order, 0], ptrs[order, 1])
+    assert len(calls) >= 3 and sum(c[1] for c in calls) == 3000
+    raw = p.read_bytes()
+    for j in range(0, 3000, 41):
+        i = int(order[j])
+        s, e = int(ptrs[i, 0]), int(ptrs[i, 1])
+        _, _, ent = orc.decode(raw[s + 12 : e - 4])
+        f = feats[j]
+        for key, kind, vals in ent:
+            got = f[key.decode()].value
+            if kind == "float_list":
+                got = np.asarray(got, np.float32).view(np.uint32).tolist()
+            assert got == vals, (j, key)

@@ -25,6 +25,25 @@ LOGGER = logging.Logger(__name__)
 
 #: host batches are split below the device limit of 4 GiB per decode call
 MAX_BATCH_BYTES = 1 << 30
+#: per-slot columns cost ~18 B per (slot, record) (order, count, loc, row splits): batches of
+#: high-cardinality (sparse) key sets are split by records so that slots x records stays bounded
+SLOT_BUDGET_BYTES = 4 << 30
+SLOT_COLUMN_BYTES = 18
+
+
+def _decode_bounded(dec, buf: np.ndarray, st: np.ndarray, en: np.ndarray):
+    """dec.decode over record chunks of at most SLOT_BUDGET_BYTES / (18 x slots) records (the slot
+    count known before each chunk; a chunk that learns many new keys only shrinks the next ones).
+    Yields (first record index, BatchResult)."""
+    n = st.size
+    at = 0
+    while at < n:
+        slots = max(1, len(dec.keys.slot_key))
+        k = max(1024, SLOT_BUDGET_BYTES // (SLOT_COLUMN_BYTES * slots))
+        if slots < 64:  # (a schema still being learned: a first chunk of bounded size)
+            k = min(k, 1 << 16)
+        yield at, dec.decode(buf, st[at : at + k], en[at : at + k])
+        at += k
 
 
 def _check_path(path) -> None:
@@ -132,7 +151,8 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
                                              N.ptr(buf[at:]) if buf.size else None)
         lens = (ends[idx] - starts[idx]).astype(np.uint64)
         b_en = np.cumsum(lens, dtype=np.uint64)
-        take(dec.decode(buf, b_en - lens, b_en), idx)
+        for at, res in _decode_bounded(dec, buf, b_en - lens, b_en):
+            take(res, idx[at : at + res.status.size])
         pend_img, pend_idx, pend_bytes = [], [], 0
 
     for path, idxs in by_file.items():
@@ -155,7 +175,8 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
             continue
         sel = int((ends[ok] - starts[ok]).sum())
         if sel * 4 >= fsize and fsize <= MAX_BATCH_BYTES:  # dense selection: the image itself
-            take(dec.decode(img, starts[ok], ends[ok]), ok)
+            for at, res in _decode_bounded(dec, img, starts[ok], ends[ok]):
+                take(res, ok[at : at + res.status.size])
             continue
         for lo in range(0, ok.size, 1 << 20):  # sparse selection: staged back to back
             part = ok[lo : lo + (1 << 20)]
