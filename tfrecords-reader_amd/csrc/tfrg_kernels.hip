@@ -1031,6 +1031,9 @@ __device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e,
   return true;
 }
 
+#ifndef TFRG_HBM_BLOCKS
+#define TFRG_HBM_BLOCKS 2
+#endif
 // count_packed over HBM (records walked from HBM): aligned 16-byte blocks, two loads in flight per
 // round instead of one dependent dword pair per word (a packed list of 300 bytes was 75 serial
 // round trips; four blocks per round would cost the staged path its occupancy in VGPRs)
@@ -1039,15 +1042,15 @@ __device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o,
   uint32_t run = 0, terms = 0;
   const uint64_t a0 = s.base + o, a1 = s.base + e;
   const uint64_t lb = s.lim - 12;  // last readable 16-byte block
-  for (uint64_t q = a0 & ~15ull; q < a1; q += 32) {
-    uint4 blk[2];
+  for (uint64_t q = a0 & ~15ull; q < a1; q += 16 * TFRG_HBM_BLOCKS) {
+    uint4 blk[TFRG_HBM_BLOCKS];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TFRG_HBM_BLOCKS; ++j) {
       const uint64_t qq = q + 16u * j;
       blk[j] = *reinterpret_cast<const uint4*>(s.buf + (qq < lb ? qq : lb));
     }
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < TFRG_HBM_BLOCKS; ++j) {
       const uint32_t ws[4] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
