@@ -280,10 +280,9 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> 
         # lane kernel: its records' framed bytes + offsets in; status, verdict, order + count per slot
         # and a location / single-value word per present list out
         "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
-        # exact walker of the slow list (empty on these workloads): its launch reads the list count
-        "k_tail_count": 64,
-        # streaming payload CRC of the records above lane_max: their bytes + list entry and offsets
-        "k_crc_stream": big_bytes + 32 * n_big,
+        # streaming payload CRC of the records above lane_max (their bytes + list entry and offsets);
+        # the exact walker's slow list is empty on these workloads
+        "k_tail_count": big_bytes + 32 * n_big,
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         # out-of-line lists: every value written once (their record bytes are counted by the lanes)

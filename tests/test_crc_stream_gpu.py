@@ -1,4 +1,4 @@
-"""Streaming payload CRC of the records above lane_max (k_crc_stream), against the oracle's CRC-32C.
+"""Streaming payload CRC of the records above lane_max (k_tail_count role 2), against the oracle's CRC-32C.
 
 The kernel numbers every listed record's 1 KiB rounds into one flat space and gives each wave an
 equal slice, so the shapes that matter are: one record split over (nearly) every wave of the grid,

@@ -180,7 +180,7 @@ struct LaunchCfg {
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageCrc, kStageSpine, kStageDownGather, kStageTailGather,
+enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageSpine, kStageDownGather, kStageTailGather,
                    kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 

@@ -1760,9 +1760,6 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
 // the slices of a record split over waves XOR together in crc_part (CRC-32C is linear, crc32c.h)
 // and the wave whose rounds complete the record finishes it.
 constexpr int kCrcDepth = TFRG_CRC_DEPTH;
-#ifndef TFRG_CRC_WAVES
-#define TFRG_CRC_WAVES 5  // waves per SIMD k_crc_stream is register-budgeted for
-#endif
 constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
 constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
 constexpr uint32_t kNumCst = 128;
@@ -2100,22 +2097,19 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   PHASE_ADD(25, q0, q9);
 }
 
-// The exact walker for the slow list before the row-split scan (usually empty: a workgroup leaves at
-// once when it has nothing to do).
+// The exception paths before the row-split scan in ONE launch (usually both empty: a workgroup leaves
+// at once when it has nothing to do): the exact walker for the slow list (role 1), then the streaming
+// payload CRC of the listed large records (role 2). The two record sets are disjoint (the lane kernel
+// lists only records it accepted), so a strict CRC rejection of role 2 never meets role 1's records.
+// (Role 2 as its own kernel at 5 instead of 4 waves per SIMD measured the same on C2: 0.129 vs 0.130
+// ms; its own launch cost every batch ~6.5 us.)
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kLaneBlock) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
-                                                           const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
+                                                           const uint32_t* __restrict__ crc_tab,
+                                                           const uint32_t* __restrict__ consts, uint32_t lane_max) {
   role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
-}
-
-// The streaming payload CRC of the large records, after the slow walker (a strict rejection reads
-// the status it wrote) and before the scan (a rejection withdraws counts). Its own launch: the slow
-// walker's registers would cost it a third of its resident waves.
-__global__ __launch_bounds__(kLaneBlock, TFRG_CRC_WAVES) void k_crc_stream(DevBatch B, DevOut o,
-                                                                          const uint32_t* __restrict__ crc_tab,
-                                                                          const uint32_t* __restrict__ consts,
-                                                                          uint32_t n_slots) {
-  role_crc_stream(B, o, crc_tab, consts, n_slots);
+  __syncthreads();  // (the LDS tables are reloaded by role 2)
+  role_crc_stream(B, o, crc_tab, consts, sc.n_slots);
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in
@@ -2869,7 +2863,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_crc_stream", "k_spine",
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -2917,24 +2911,20 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageTailCount);
-  // the exact walker for the slow list (usually empty): grid-stride, a workgroup leaves at once when
-  // it has nothing to do
+  // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
+  // the large payloads evenly over the waves; role 1 grid-strides over the slow list)
   {
     const bool gord = slow_lds > kLaneLdsBudget;
-    const size_t lds = gord ? 2048ull * 4 : slow_lds;
-    const uint32_t g = b.n < (uint32_t)cfg.num_cus * 8u ? (b.n ? b.n : 1u) : (uint32_t)cfg.num_cus * 8u;
+    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_lds, (5120 + kNumCst) * 4);
+    const void* fn = gord ? reinterpret_cast<const void*>(&k_tail_count<COMPAT, true>)
+                          : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
+    const uint32_t g = (uint32_t)resident_grid(fn, lds, false);
     if (gord)
-      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab, d_consts,
                          cfg.lane_max);
     else
       hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
-                         cfg.lane_max);
-  }
-  mark(kStageCrc);
-  {  // one round of resident workgroups: the large payloads split evenly over the waves
-    const size_t lds = (5120 + kNumCst) * 4;
-    const uint32_t g = (uint32_t)resident_grid(reinterpret_cast<const void*>(&k_crc_stream), lds, false);
-    hipLaunchKernelGGL(k_crc_stream, dim3(g), dim3(kLaneBlock), lds, st, b, o, d_tab, d_consts, (uint32_t)S);
+                         d_consts, cfg.lane_max);
   }
   mark(kStageSpine);
   if (S > 0)
