@@ -95,6 +95,11 @@ struct tfrg_ctx {
   uint32_t n_tpl = 0;
   bool tpl_learned = false;
   bool tpl_on = true;
+  // speculative single-value placement (DevSchema::spec), derived from the templates
+  std::vector<uint8_t> slot_kind_h;
+  DBuf spec;
+  bool have_spec = false;
+  bool spec_on = true;
   // optional per-stage HIP events (tfrg_ctx_set_profiling)
   bool profiling = false;
   bool have_events = false;
@@ -115,6 +120,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   tfrg_ctx* c = new tfrg_ctx();
   c->device = device;
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
+  if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -156,7 +162,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
-                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl};
+                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec};
   for (DBuf* b : all) b->release();
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
@@ -277,8 +283,10 @@ int tfrg_set_schema(tfrg_ctx* c, uint32_t n_keys, const uint8_t* key_blob, const
   for (uint32_t k = 0; k < n_keys; ++k)
     c->key_id.emplace(std::string((const char*)key_blob + key_offsets[k], key_offsets[k + 1] - key_offsets[k]), k);
   c->key_slot_h = ks;
+  c->slot_kind_h.assign(slot_kind, slot_kind + n_slots);
   c->n_tpl = 0;  // slots may have moved: learn again from the next host batch
   c->tpl_learned = false;
+  c->have_spec = false;
   return 0;
 }
 
@@ -297,6 +305,7 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.krec = c->krec.as<uint32_t>();
   s.tpl = c->tpl.as<uint32_t>();
   s.n_tpl = c->tpl_on ? c->n_tpl : 0u;
+  s.spec = c->tpl_on && c->spec_on && c->have_spec && c->n_tpl ? c->spec.as<uint32_t>() : nullptr;
   return s;
 }
 
@@ -420,6 +429,7 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   if (!c || (n && (!h_bytes || !h_start || !h_end))) return TFRG_E_ARG;
   c->tpl_learned = true;
   c->n_tpl = 0;
+  c->have_spec = false;
   if (!c->n_keys) return 0;
   std::map<std::string, std::pair<uint32_t, Tpl>> seen;  // shape -> (records, template)
   Tpl t;
@@ -464,6 +474,37 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   }
   HIP_TRY(hipMemcpy(c->tpl.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
   c->n_tpl = nt;
+  // speculative placement (DevSchema::spec): slots that are an inline single value in every kept
+  // template, taken per kind in slot order up to the first slot of that kind that is not one (its
+  // column base n * rank then holds whenever every record is regular)
+  const uint32_t S = c->n_slots;
+  std::vector<uint32_t> seen_inline(S, 0), spec(S ? S : 1, 0);
+  for (uint32_t k = 0; k < nt; ++k) {
+    const Tpl& x = *order[k].second;
+    for (size_t e = 0; e < x.ent.size(); e += 4) {
+      const uint32_t slot = x.ent[e] & 0xffffffu, mode = x.ent[e] >> 24;
+      if (mode && slot < S) ++seen_inline[slot];
+    }
+  }
+  uint32_t rank[4] = {0, 0, 0, 0};
+  bool open[4] = {true, true, true, true};
+  for (uint32_t k = 0; k < S; ++k) {
+    const uint32_t kd = c->slot_kind_h[k] & 3u;
+    if (!open[kd]) continue;
+    if (seen_inline[k] == nt) {
+      spec[k] = ((++rank[kd]) << 2) | kd;
+      c->have_spec = true;
+    } else {
+      open[kd] = false;
+    }
+  }
+  if (c->have_spec) {
+    if (c->spec.ensure((size_t)S * 4)) {
+      set_error("template allocation failed");
+      return TFRG_E_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(c->spec.p, spec.data(), (size_t)S * 4, hipMemcpyHostToDevice));
+  }
   return (int)nt;
 }
 
@@ -502,7 +543,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   const uint32_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
   const uint32_t tile_stride = (n_tiles + 3u) & ~3u;
   const uint32_t n_chunks = (n_tiles + (1u << kSpineChunkShift) - 1u) >> kSpineChunkShift;
-  const uint64_t tsum_words = (uint64_t)S * tile_stride + 2ull * S * n_chunks;  // tile sums + look-back words
+  // tile sums + look-back words + per-slot irregular-record counts (DevOut::irr)
+  const uint64_t tsum_words = (uint64_t)S * tile_stride + 2ull * S * n_chunks + S;
   // value capacities: bounds for disjoint ranges (one int64 per byte, one float per 4, one bytes
   // element per 2); tfrg_decode_host passes the total of its ranges, which covers overlaps. A batch
   // of overlapping device ranges that exceeds them is reported by tfrg_result_info (TFRG_E_LIMIT).
@@ -587,6 +629,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.tile_stride = tile_stride;
   o.spine_lb = reinterpret_cast<uint64_t*>(o.tsum + (size_t)S * tile_stride);  // 16-byte aligned
   o.n_chunks = n_chunks;
+  o.irr = o.tsum + (size_t)S * tile_stride + 2ull * S * n_chunks;
   o.slow_list = c->slow_list.as<uint32_t>();
   o.crc_rec = c->crc_rec.as<uint32_t>();
   o.crc_base = c->crc_base.as<uint64_t>();

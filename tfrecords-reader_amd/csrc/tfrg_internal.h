@@ -22,6 +22,12 @@ struct DevSchema {
   const uint32_t* krec;        // [n_keys][8] packed key record, see KeyRec
   const uint32_t* tpl;         // [n_tpl][kTplWords] record-shape templates (below), learned on the host
   uint32_t n_tpl;
+  // [n_slots] speculative placement of single values (null = off): 0, or (rank + 1) << 2 | kind for
+  // a slot that is an inline single value in every learned template, as are all slots of its kind
+  // before it. The lane kernel then writes such a value straight to its column at n * rank + r and
+  // the row split r; k_down_gather skips the slot when every record was regular (irr == 0) and the
+  // slot's column base is n * rank, i.e. when that placement is the final one.
+  const uint32_t* spec;
 };
 
 // Record-shape template: the payload of a canonical record whose every byte except list contents is
@@ -134,6 +140,8 @@ struct DevOut {
   uint32_t* crc_rec;     // [n] streaming-CRC list: record
   uint64_t* crc_base;    // [n] its first flat round (ascending with the list index)
   uint64_t* crc_part;    // [n] rounds done << 32 | XOR of the slices, of a record split over waves
+  uint32_t* irr;         // [n_slots] records not placed speculatively per slot (DevSchema::spec; after
+                         // the scan words in their buffer, zero between decodes: k_tail_gather clears)
 };
 
 // Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)

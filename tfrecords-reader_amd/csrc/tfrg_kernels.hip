@@ -343,6 +343,18 @@ __device__ int walk_example(S& s, Sink& sink, int64_t& aux) {
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
 
+// single value stored in the loc word by the count pass
+__device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2 lc, uint64_t dst) {
+  if (kind == TFRG_KIND_INT64) {
+    if (dst < o.cap_i64) o.i64[dst] = (int64_t)(((uint64_t)lc.y << 32) | lc.x);
+  } else if (kind == TFRG_KIND_FLOAT) {
+    if (dst < o.cap_f32) o.f32[dst] = lc.x;
+  } else if (dst < o.cap_b) {
+    o.b_off[dst] = lc.x;
+    o.b_len[dst] = lc.y;
+  }
+}
+
 template <bool L>
 struct CountSinkT {
   using ord_t = std::conditional_t<L, lds_u16, uint16_t>;
@@ -358,6 +370,7 @@ struct CountSinkT {
   bool miss;
   bool leader;       // issues global writes and atomics
   cnt_t* cnt = nullptr;  // LDS value counts, same layout as ord (L only)
+  const lds_u32* spec = nullptr;  // DevSchema::spec staged in LDS (L only; null = off)
 
   __device__ __forceinline__ void reset() {
     for (uint32_t k = 0; k < sc->n_slots; ++k) ord[(size_t)k * ostride] = 0;
@@ -455,6 +468,16 @@ struct CountSinkT {
     const size_t at = (size_t)slot * n + r;
     if constexpr (L) cnt[(size_t)slot * ostride] = cw;
     else o->count[at] = cw;
+    if constexpr (L) {
+      if (spec) {  // speculative placement of a single value (DevSchema::spec): no loc word (k_spine
+                   // copies the value back into it if the slot's placement fails)
+        const uint32_t sw = spec[slot];
+        if (sw && (cw & kCountInline)) {
+          put_inline(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u) + r);
+          return;
+        }
+      }
+    }
     o->loc[at] = lv;
   }
 
@@ -534,6 +557,11 @@ struct MaskSink {
 // ------------------------------------------------------------------------------------------------
 // LDS table view with R-fold bank replication: entry (j, v) copy c at dword ((j*256+v)*R + c).
 // Lane l reads copy l % R, so up to R lanes of a 32-lane group never collide on a bank.
+// a ^ b ^ c in one VALU (gfx950 v_bitop3_b32, truth table 0x96; the compiler does not fuse XOR chains)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 // ((x >> 8K) & 0xff) * 4 in one VALU: a shift with an SDWA byte select of its source
 template <int K>
 __device__ __forceinline__ uint32_t byte_x4(uint32_t x) {
@@ -1484,6 +1512,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
   uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneBlock / 64) * 64u : 0u);  // templates
+  uint32_t* spec_l = tpl_l + sc.n_tpl * kTplWords;  // MODE 0: DevSchema::spec
   for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
   if constexpr (MODE == 1) {
     tsl[lane] = 0;
@@ -1494,6 +1523,9 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
     for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneBlock) tpl_l[i] = sc.tpl[i];
   }
+  const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
+  if (spec_on)
+    for (uint32_t i = threadIdx.x; i < S; i += kLaneBlock) spec_l[i] = sc.spec[i];
   __syncthreads();
   const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
@@ -1552,7 +1584,10 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       } else {
         CountSinkT<MODE == 0> c{&sc, &o, dict_ord<MODE == 0>(o.order + r, ord + threadIdx.x),
                                 GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
-        if constexpr (MODE == 0) c.cnt = (lds_u32*)(cnt + threadIdx.x);
+        if constexpr (MODE == 0) {
+          c.cnt = (lds_u32*)(cnt + threadIdx.x);
+          if (spec_on) c.spec = (const lds_u32*)spec_l;
+        }
         return c;
       }
     }();
@@ -1644,6 +1679,11 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       if (nz) {  // counts of 0/1 (single values): the sum is a popcount of the ballot (scalar)
         const uint32_t t = __ballot(x > 1u) ? wave_sum_u32(x) : (uint32_t)__popcll(nz);
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
+      }
+      if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
+        if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
+        const uint64_t irm = __ballot(valid && !(done && c == (1u | kCountInline)));
+        if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
       }
     }
     }
@@ -1803,11 +1843,16 @@ __device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uin
 // drained them in two halves), in a single asm block so that no result is read before the wait.
 // Each read overwrites its own address register (16 VGPRs, not 32).
 __device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
-  uint32_t r0 = byte_x4<0>(w.x), r1 = byte_x4<1>(w.x), r2 = byte_x4<2>(w.x), r3 = byte_x4<3>(w.x);
-  uint32_t r4 = byte_x4<0>(w.y), r5 = byte_x4<1>(w.y), r6 = byte_x4<2>(w.y), r7 = byte_x4<3>(w.y);
-  uint32_t r8 = byte_x4<0>(w.z), r9 = byte_x4<1>(w.z), r10 = byte_x4<2>(w.z), r11 = byte_x4<3>(w.z);
-  uint32_t r12 = byte_x4<0>(w.w), r13 = byte_x4<1>(w.w), r14 = byte_x4<2>(w.w), r15 = byte_x4<3>(w.w);
+  // byte extraction inside the block too: left to the scheduler, the 16 offsets of every chunk of a
+  // group were computed ahead of the first read (64 live VGPRs, spills)
+  uint32_t r[16];
+  const uint32_t two = 2u;
+#define TFRG_SDWA(o, two, src, k) "v_lshlrev_b32_sdwa %" #o ", %" #two ", %" #src " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_" #k "\n\t"
   asm volatile(
+      TFRG_SDWA(0, 16, 17, 0) TFRG_SDWA(1, 16, 17, 1) TFRG_SDWA(2, 16, 17, 2) TFRG_SDWA(3, 16, 17, 3)
+      TFRG_SDWA(4, 16, 18, 0) TFRG_SDWA(5, 16, 18, 1) TFRG_SDWA(6, 16, 18, 2) TFRG_SDWA(7, 16, 18, 3)
+      TFRG_SDWA(8, 16, 19, 0) TFRG_SDWA(9, 16, 19, 1) TFRG_SDWA(10, 16, 19, 2) TFRG_SDWA(11, 16, 19, 3)
+      TFRG_SDWA(12, 16, 20, 0) TFRG_SDWA(13, 16, 20, 1) TFRG_SDWA(14, 16, 20, 2) TFRG_SDWA(15, 16, 20, 3)
       "ds_read_b32 %0, %0 offset:15360\n\t"
       "ds_read_b32 %1, %1 offset:14336\n\t"
       "ds_read_b32 %2, %2 offset:13312\n\t"
@@ -1825,14 +1870,33 @@ __device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
       "ds_read_b32 %14, %14 offset:1024\n\t"
       "ds_read_b32 %15, %15\n\t"
       "s_waitcnt lgkmcnt(0)"
-      : "+v"(r0), "+v"(r1), "+v"(r2), "+v"(r3), "+v"(r4), "+v"(r5), "+v"(r6), "+v"(r7), "+v"(r8), "+v"(r9),
-        "+v"(r10), "+v"(r11), "+v"(r12), "+v"(r13), "+v"(r14), "+v"(r15));
-  return ((r0 ^ r1) ^ (r2 ^ r3)) ^ ((r4 ^ r5) ^ (r6 ^ r7)) ^ ((r8 ^ r9) ^ (r10 ^ r11)) ^
-         ((r12 ^ r13) ^ (r14 ^ r15));
+      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
+        "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
+        "=&v"(r[15])
+      : "v"(two), "v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
+  return xor3(xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], r[8])),
+              xor3(r[9], r[10], r[11]), xor3(r[12], r[13], r[14])) ^ r[15];
 }
 
 __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
   return M[S & 0xffu] ^ M[256 + ((S >> 8) & 0xffu)] ^ M[512 + ((S >> 16) & 0xffu)] ^ M[768 + (S >> 24)];
+}
+
+// mul_tab of the x^8192 table A1 at LDS byte 16384 (after the slice-by-16 tables at 0), with SDWA
+// byte offsets and immediate table offsets: 4 VALU + 4 LDS reads + 2 XOR
+__device__ __forceinline__ uint32_t mul_a1_lds(uint32_t S) {
+  uint32_t m0, m1, m2, m3;
+  const uint32_t two = 2u;
+  asm volatile(
+      TFRG_SDWA(0, 4, 5, 0) TFRG_SDWA(1, 4, 5, 1) TFRG_SDWA(2, 4, 5, 2) TFRG_SDWA(3, 4, 5, 3)
+      "ds_read_b32 %0, %0 offset:16384\n\t"
+      "ds_read_b32 %1, %1 offset:17408\n\t"
+      "ds_read_b32 %2, %2 offset:18432\n\t"
+      "ds_read_b32 %3, %3 offset:19456\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)
+      : "v"(two), "v"(S));
+  return xor3(m0, m1, m2) ^ m3;
 }
 
 // TFRG_FLAG_STRICT_CRC, payload CRC of a record above lane_max failed: the record becomes an error
@@ -1847,6 +1911,7 @@ __device__ void strict_reject(const DevOut& o, uint32_t n, uint32_t n_slots, uin
     if (o.order[at]) o.order[at] = 0;  // (present slots with empty lists have count 0)
     if (!c) continue;
     o.count[at] = 0;
+    atomicAdd(&o.irr[k], 1u);  // (a speculatively placed value is withdrawn: k_down_gather places the slot)
     if (c & ~kCountInline) atomicSub(&o.tsum[(size_t)k * o.tile_stride + (r >> kTileShift)], c & ~kCountInline);
   }
   if (t == 0) {
@@ -1874,13 +1939,12 @@ __device__ __forceinline__ uint32_t xpow_rounds(uint32_t j, const uint32_t* cst,
 }
 
 // The streaming-CRC window: lane k < 63 describes list entry win0 + k, lane 63 holds the next
-// window's first flat round (the bound of this one).
+// window's first flat round (the bound of this one). Three 64-bit values per lane; everything else
+// about an entry is derived in scalar registers (crc_ent) or loaded at its flush: the fewer VGPRs,
+// the more group loads in flight without spills.
 struct CrcWin {
-  uint64_t base;    // first flat round
-  uint64_t E;       // chunk of flat round R, lane l: E + 64 R - l
-  uint64_t c0;      // first payload chunk
-  uint64_t a, b;    // payload [a, b)
-  uint32_t J, r, verdict, stored;
+  uint64_t base;  // first flat round (entry k's rounds: [base[k], base[k + 1]))
+  uint64_t a, b;  // payload [a, b)
 };
 
 __device__ __forceinline__ CrcWin crc_win_load(const DevBatch& B, const DevOut& o, uint32_t win0, uint32_t nrec,
@@ -1889,21 +1953,29 @@ __device__ __forceinline__ CrcWin crc_win_load(const DevBatch& B, const DevOut& 
   const uint32_t idx = win0 + lane;
   w.base = idx < nrec ? o.crc_base[idx] : TR;
   if (idx < nrec && lane < 63u) {
-    w.r = o.crc_rec[idx];
-    const RecView v = rec_view(B, w.r);
+    const RecView v = rec_view(B, o.crc_rec[idx]);
     w.a = v.p0;
     w.b = v.e - 4;
-    w.verdict = o.verdict[w.r];
-    w.stored = load_u32_unaligned(B.bytes, w.b);
-    const uint64_t c1 = (w.b - 1) >> 4;
-    w.c0 = w.a >> 4;
-    w.J = (uint32_t)((c1 - w.c0 + 64) >> 6);
-    w.E = c1 - 64ull * (w.J - 1u) - 64ull * w.base;
   }
   // the window's loads retired here: the group loads issued after it then carry no false wait on
   // them (a merged loop-header state otherwise drains vmcnt before every group)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   return w;
+}
+
+// (scalar) window entry k: first round, round count J, chunk of its round R for lane l (E + 64 R - l;
+// the rounds end at the payload's last chunk c1), first payload chunk c0
+struct CrcEnt {
+  uint64_t bas, J, E, c0;
+};
+__device__ __forceinline__ CrcEnt crc_ent(const CrcWin& w, uint32_t k) {
+  CrcEnt e;
+  e.bas = rl64(w.base, k);
+  e.J = rl64(w.base, k + 1u) - e.bas;
+  const uint64_t c1 = (rl64(w.b, k) - 1u) >> 4;
+  e.E = c1 - 64ull * (e.J - 1u) - 64ull * e.bas;
+  e.c0 = rl64(w.a, k) >> 4;
+  return e;
 }
 
 // the rounds [Rf, Rl] of window entry k, Horner sum S per lane: placed, combined with the other
@@ -1912,7 +1984,7 @@ __device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, co
                                        uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
                                        uint32_t n_slots, uint32_t lane) {
   const uint64_t bas = rl64(w.base, k);
-  const uint32_t J = rl32(w.J, k);
+  const uint32_t J = (uint32_t)(rl64(w.base, k + 1u) - bas);
   const uint32_t jtop = J - 1u - (uint32_t)(Rf - bas), jlo = J - 1u - (uint32_t)(Rl - bas);
   uint32_t t = gf_mul(S, cst[lane]);
 #pragma unroll
@@ -1940,10 +2012,10 @@ __device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, co
     t ^= (uint32_t)seen;
   }
   const uint64_t b = rl64(w.b, k);
-  const uint32_t r = rl32(w.r, k), verdict = rl32(w.verdict, k);
+  const uint32_t r = rfl32(o.crc_rec[win0 + k]), verdict = o.verdict[r];
   const uint32_t z = (uint32_t)(16ull * (((b - 1) >> 4) + 1ull) - b);  // zero bytes padding the last chunk
   const uint32_t c = ~gf_mul(t, cst[kCstUnshift + z]);
-  if (crc_mask(c) == rl32(w.stored, k)) {
+  if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) {
     if (lane == 0) o.verdict[r] = (uint8_t)(verdict | TFRG_V_DATA_CRC);
   } else if (B.flags & kFlagStrictCrc) {
     strict_reject(o, B.n, n_slots, r, verdict, lane, 64);
@@ -2007,8 +2079,9 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
       g.rd[d] = Rs + ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u);
       g.kd[d] = (uint32_t)__popcll(__ballot(w.base <= g.rd[d])) - 1u;
-      const uint64_t c0 = rl64(w.c0, g.kd[d]);
-      const uint64_t ch = rl64(w.E, g.kd[d]) + 64ull * g.rd[d] - lane;
+      const CrcEnt e = crc_ent(w, g.kd[d]);
+      const uint64_t c0 = e.c0;
+      const uint64_t ch = e.E + 64ull * g.rd[d] - lane;
       g.wd[d] = *reinterpret_cast<const uint4*>(B.bytes + (((int64_t)ch >= (int64_t)c0 ? ch : c0) << 4));
     }
   };
@@ -2023,7 +2096,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
 #pragma unroll
     for (int d = 0; d < kCrcDepth; ++d) {
       const uint64_t bas = rl64(w.base, g.kd[d]);
-      edge |= g.rd[d] <= bas + 1u || g.rd[d] == bas + rl32(w.J, g.kd[d]) - 1u;
+      edge |= g.rd[d] <= bas + 1u || g.rd[d] == rl64(w.base, g.kd[d] + 1u) - 1u;
     }
     if (!edge && tab_at0) {  // interior group: one LDS round trip per chunk
 #pragma unroll
@@ -2034,12 +2107,11 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     } else {
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) {
-        const uint64_t bas = rl64(w.base, g.kd[d]);
-        const uint32_t J = rl32(w.J, g.kd[d]);
-        if (g.rd[d] <= bas + 1u || g.rd[d] == bas + J - 1u) {
-          const uint64_t ch = rl64(w.E, g.kd[d]) + 64ull * g.rd[d] - lane;
+        const CrcEnt e = crc_ent(w, g.kd[d]);
+        if (g.rd[d] <= e.bas + 1u || g.rd[d] == e.bas + e.J - 1u) {
+          const uint64_t ch = e.E + 64ull * g.rd[d] - lane;
           const uint64_t a = rl64(w.a, g.kd[d]), b = rl64(w.b, g.kd[d]);
-          rc[d] = (int64_t)ch >= (int64_t)rl64(w.c0, g.kd[d]) ? chunk_u(g.wd[d], ch << 4, a, b, T) : 0u;
+          rc[d] = (int64_t)ch >= (int64_t)e.c0 ? chunk_u(g.wd[d], ch << 4, a, b, T) : 0u;
         } else {
           rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);  // (interior: no masks)
         }
@@ -2104,7 +2176,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
 // (Role 2 as its own kernel at 5 instead of 4 waves per SIMD measured the same on C2: 0.129 vs 0.130
 // ms; its own launch cost every batch ~6.5 us.)
 template <bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kLaneBlock) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneBlock, 4) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            const uint32_t* __restrict__ consts, uint32_t lane_max) {
   role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
@@ -2188,9 +2260,27 @@ __device__ __forceinline__ uint32_t spine_look_back(const uint64_t* lb, uint32_t
   return excl;
 }
 
-// grid n_chunks * n_slots (1-D)
+// DevSchema::spec: the speculative placement of slot k is not final -- some record of it or of an
+// earlier slot of its kind (all speculative: they form a prefix) was irregular. Otherwise every such
+// slot holds n values at rows 0..n-1, so the column base of slot k is n * rank, as placed.
+__device__ __forceinline__ bool spec_failed(const uint32_t* spec, const DevOut& o, uint32_t k) {
+  const uint32_t sw = spec ? spec[k] : 0u;
+  if (!sw) return false;
+  for (uint32_t j = 0; j <= k; ++j) {
+    const uint32_t sj = spec[j];
+    if (sj && ((sj ^ sw) & 3u) == 0u && o.irr[j]) return true;
+  }
+  return false;
+}
+__device__ __forceinline__ bool spec_placed(const uint32_t* spec, const DevOut& o, uint32_t k) {
+  return spec && spec[k] && !spec_failed(spec, o, k);
+}
+
+// grid n_chunks * n_slots (1-D). With DevSchema::spec, a workgroup of a slot whose speculative
+// placement failed first copies the placed single values of its chunk's records back into their loc
+// words (value columns -> loc: no overlap with k_down_gather's writes, which follow this kernel).
 __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* __restrict__ slot_kind, uint32_t n_slots,
-                                                       uint32_t n_tiles) {
+                                                       uint32_t n_tiles, const uint32_t* __restrict__ spec, uint32_t n) {
   __shared__ uint32_t s_w[kSpineBlock / 64];
   __shared__ uint32_t s_ticket, s_excl, s_last;
   __shared__ uint32_t s_w2[kSpineBlock];  // last workgroup: slot totals of one pass
@@ -2199,6 +2289,29 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
   if (threadIdx.x == 0) s_ticket = atomicAdd(&o.info[kInfoSpineTicket], 1u);
   __syncthreads();
   const uint32_t slot = s_ticket / o.n_chunks, chunk = s_ticket % o.n_chunks;
+  if (spec_failed(spec, o, slot)) {  // (workgroup-uniform; rare: an irregular batch)
+    const uint32_t sw = spec[slot];
+    const uint64_t sb = (uint64_t)n * ((sw >> 2) - 1u);
+    const uint64_t r0 = (uint64_t)chunk << (kSpineChunkShift + kTileShift);
+    const uint64_t r1 = r0 + (1ull << (kSpineChunkShift + kTileShift)) < n ? r0 + (1ull << (kSpineChunkShift + kTileShift)) : n;
+    for (uint64_t r = r0 + threadIdx.x; r < r1; r += kSpineBlock) {
+      const size_t at = (size_t)slot * n + r;
+      if (o.count[at] != (1u | kCountInline)) continue;
+      const uint64_t p = sb + r;
+      uint2 lv = make_uint2(0, 0);
+      if ((sw & 3u) == TFRG_KIND_INT64) {
+        if (p < o.cap_i64) {
+          const uint64_t v = (uint64_t)o.i64[p];
+          lv = make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+        }
+      } else if ((sw & 3u) == TFRG_KIND_FLOAT) {
+        if (p < o.cap_f32) lv.x = o.f32[p];
+      } else if (p < o.cap_b) {
+        lv = make_uint2(o.b_off[p], o.b_len[p]);
+      }
+      o.loc[at] = lv;
+    }
+  }
   uint32_t* t = o.tsum + (size_t)slot * o.tile_stride;
   uint64_t* lb = o.spine_lb + (size_t)slot * o.n_chunks;
   const uint32_t i0 = (chunk << kSpineChunkShift) + threadIdx.x * kSpineItems;
@@ -2377,18 +2490,6 @@ __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema
   }
 }
 
-// single value stored in the loc word by the count pass
-__device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2 lc, uint64_t dst) {
-  if (kind == TFRG_KIND_INT64) {
-    if (dst < o.cap_i64) o.i64[dst] = (int64_t)(((uint64_t)lc.y << 32) | lc.x);
-  } else if (kind == TFRG_KIND_FLOAT) {
-    if (dst < o.cap_f32) o.f32[dst] = lc.x;
-  } else if (dst < o.cap_b) {
-    o.b_off[dst] = lc.x;
-    o.b_len[dst] = lc.y;
-  }
-}
-
 // Row-split scan, last level, fused with the lane-record gather. One workgroup per 256-record tile:
 // per slot, the tile prefix (k_spine) + the in-tile exclusive scan of the counts give the row splits;
 // single values kept inline by the count pass are written straight from the loc word, other lists of
@@ -2418,7 +2519,17 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
   // with the slot present (failed records and absent slots have count 0).
   uint32_t need = 0;  // bit t: record r[t] has an out-of-line list
   uint32_t buf = 0;
-  for (uint32_t k0 = 0; k0 < S; k0 += kDG, buf ^= 1u) {
+  // slots whose speculative placement by the lane kernel is final (DevSchema::spec): nothing to do
+  auto placed = [&](uint32_t k) -> bool { return k < S && spec_placed(sc.spec, o, k); };
+  for (uint32_t k0 = 0; k0 < S; k0 += kDG) {
+    bool sk[kDG];
+    bool all = true;
+#pragma unroll
+    for (uint32_t g = 0; g < kDG; ++g) {
+      sk[g] = placed(k0 + g);
+      all &= sk[g] || k0 + g >= S;
+    }
+    if (all) continue;  // (workgroup-uniform; buf toggles only with a barrier)
     uint32_t c[kDT][kDG], ex[kDT][kDG];
     uint2 lc[kDT][kDG];
 #pragma unroll
@@ -2426,7 +2537,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
 #pragma unroll
       for (uint32_t g = 0; g < kDG; ++g) {
         const uint32_t k = k0 + g < S ? k0 + g : k0;
-        const bool in = valid[t] && k0 + g < S;
+        const bool in = valid[t] && k0 + g < S && !sk[g];
         c[t][g] = in ? o.count[(size_t)k * B.n + r[t]] : 0u;
         lc[t][g] = in ? o.loc[(size_t)k * B.n + r[t]] : make_uint2(0, 0);
       }
@@ -2448,6 +2559,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
     for (uint32_t g = 0; g < kDG; ++g) {
       const uint32_t k = k0 + g;
       if (k >= S) break;
+      if (sk[g]) continue;
       const uint32_t kind = sc.slot_kind[k];
       const uint64_t sbase = o.slot_base[k];
 #pragma unroll
@@ -2461,6 +2573,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
         else if (c[t][g]) need |= 1u << t;
       }
     }
+    buf ^= 1u;
   }
   // records with an out-of-line list: k_list_gather (kept out of this kernel so its register
   // budget stays that of the scan); larger records are skipped there (wavefront gathers)
@@ -2851,6 +2964,8 @@ __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchem
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
+  if (blockIdx.x == 0)  // (read by k_down_gather, which has finished: zero for the next decode)
+    for (uint32_t k = threadIdx.x; k < sc.n_slots; k += kWaveBlock) o.irr[k] = 0u;
   role_list_gather<COMPAT>(B, sc, o, lane_max, stage);
   role_stage_gather<COMPAT>(B, sc, o, stage);
   role_wave_gather<COMPAT>(B, sc, o);
@@ -2882,7 +2997,11 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   const size_t keys_lds = fast_ok ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
   const size_t tpl_lds = fast_ok ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (after the MODE 1 tile sums)
-  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + tpl_lds;
+  const size_t spec_lds = fast_ok && sc.spec ? r16(S * 4) : 0;               // (MODE 0 only)
+  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + tpl_lds + spec_lds;
+  // speculative placement only with the per-lane LDS dict (MODE 0); the later kernels see the same
+  DevSchema scx = sc;
+  if (lane_lds > kLaneLdsBudget || !fast_ok) scx.spec = nullptr;
   const size_t slow_lds = 2048ull * 4 + dict_lane;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
 
@@ -2898,17 +3017,17 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
-                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
   } else if (S <= 64) {
     const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
-                       st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
   } else {
     const size_t lds = stage_lds + keys_lds + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
-                       st, b, sc, o, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageTailCount);
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
@@ -2920,22 +3039,23 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                           : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
     const uint32_t g = (uint32_t)resident_grid(fn, lds, false);
     if (gord)
-      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab, d_consts,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, scx, o, d_tab, d_consts,
                          cfg.lane_max);
     else
-      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, sc, o, d_tab,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, scx, o, d_tab,
                          d_consts, cfg.lane_max);
   }
   mark(kStageSpine);
   if (S > 0)
-    hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles);
+    hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles,
+                       scx.spec, b.n);
   mark(kStageDownGather);
   if (S > 0) {
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus)
-      hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3((n_tiles + 3) / 4), dim3(kLaneBlock), 0, st, b, sc, o,
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3((n_tiles + 3) / 4), dim3(kLaneBlock), 0, st, b, scx, o,
                          cfg.lane_max, n_tiles);
     else
-      hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles), dim3(kLaneBlock), 0, st, b, sc, o, cfg.lane_max,
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles), dim3(kLaneBlock), 0, st, b, scx, o, cfg.lane_max,
                          n_tiles);
   }
   mark(kStageTailGather);
@@ -2946,7 +3066,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
-    hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, sc, o, cfg.lane_max);
+    hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, cfg.lane_max);
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)
   return hipGetLastError();

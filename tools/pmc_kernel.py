@@ -4,9 +4,8 @@
 usage: pmc_kernel.py <outdir> <only> <kernel-substring>
 Runs two rocprofv3 --pmc passes (each within the SQ block's 8 slots, MI355X_MICROARCH.md §counters)
 over `bench.py --only <only> --no-cpu --steps 3 --warmup 1 --profile-steps 1` and prints the mean
-per full-batch launch of the kernel (largest grid, long dispatches), plus derived per-wave figures.
+per full-batch launch of the kernel (tools/_dispatch.py), plus derived per-wave figures.
 """
-import csv
 import json
 import os
 import subprocess
@@ -15,6 +14,8 @@ from collections import defaultdict
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "tools"))
+from _dispatch import full_batch_rows  # noqa: E402
 SETS = [
     "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES",
     "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT "
@@ -33,19 +34,9 @@ def main() -> None:
                "--no-cpu", "--steps", "3", "--warmup", "1", "--profile-steps", "1"]
         with open(out / f"p{i}.log", "w") as log:
             subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=dict(os.environ, TMPDIR="/tmp"))
-        rows = [r for r in csv.DictReader(open(next(d.rglob("*counter_collection.csv")))) if want in r["Kernel_Name"]]
-        gkey = "Grid_Size_X" if "Grid_Size_X" in rows[0] else "Grid_Size"
-        grid = max(int(r[gkey]) for r in rows)
-        by = defaultdict(list)
-        for r in rows:
-            if int(r[gkey]) == grid:
-                by[(r["Dispatch_Id"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))].append(r)
-        longest = max(k[1] for k in by)
         per = defaultdict(list)
-        for (did, dur), rs in by.items():
-            if dur * 2 >= longest:
-                for r in rs:
-                    per[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for r in full_batch_rows(next(d.rglob("*counter_collection.csv")), want):
+            per[r["Counter_Name"]].append(float(r["Counter_Value"]))
         for k, v in per.items():
             vals[k] = sum(v) / len(v)
     w = vals.get("SQ_WAVES", 1.0)

@@ -4,12 +4,11 @@
 usage (GPU box): pmc_traffic.py <outdir> <only> [kernel-substring]
 Runs `rocprofv3 --pmc FETCH_SIZE` and `--pmc WRITE_SIZE` (separate passes, MI355X_MICROARCH.md
 §HBM) over `bench.py --only <only> --no-cpu --steps 3 --warmup 1` (<only>: c4, c1file, c2, c3,
-c4c2), keeps the dispatches of the kernel over the full batch (largest grid), and writes
+c4c2), keeps the dispatches of the kernel over the full batch (tools/_dispatch.py), and writes
 <outdir>/traffic_<workload>.json (bench.py's workload names: c4_c1, c1file, c2, c3, c4_c2) with the
 per-launch bytes: FETCH_SIZE x 1024 x 2 (gfx950 tallies 128-B fills at 64 B: the guide's correction
 for 16-B-per-lane reads) + WRITE_SIZE x 1024. bench.py reports it as roofline.traffic.
 """
-import csv
 import json
 import os
 import subprocess
@@ -17,6 +16,8 @@ import sys
 from pathlib import Path
 
 REPO = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(REPO / "tools"))
+from _dispatch import full_batch_rows  # noqa: E402
 
 
 def run_pass(out: Path, counter: str, config: str) -> Path:
@@ -31,15 +32,9 @@ def run_pass(out: Path, counter: str, config: str) -> Path:
 
 
 def per_launch(path: Path, want: str) -> tuple[str, float]:
-    """Mean counter value over the full-batch dispatches of the kernel: the largest grid, and of
-    those the ones lasting at least half the longest (a resident-grid kernel has the same grid on
-    bench.py's small sample batch, which would otherwise be averaged in)."""
-    rows = [r for r in csv.DictReader(open(path)) if want in r["Kernel_Name"]]
-    grid = max(int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]) for r in rows)
-    rows = [r for r in rows if int(r["Grid_Size_X"] if "Grid_Size_X" in r else r["Grid_Size"]) == grid]
-    dur = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
-    vals = [float(r["Counter_Value"]) for r, d in zip(rows, dur) if d * 2 >= max(dur)]
-    return rows[0]["Kernel_Name"], sum(vals) / len(vals)
+    """Mean counter value over the full-batch dispatches of the kernel (tools/_dispatch.py)."""
+    rows = full_batch_rows(path, want)
+    return rows[0]["Kernel_Name"], sum(float(r["Counter_Value"]) for r in rows) / len(rows)
 
 
 def main() -> None:

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
-# Full GPU-box check for a round: gpu tests, smoke, default bench (with CPU baseline), c2/c3
-# benches, and a rocprofv3 kernel-trace summary of the default bench.
+# Full GPU-box check for a round: gpu tests, smoke, default bench (with CPU baseline; it also
+# runs the c1file/c2/c3/c4c2 lines under "configs"), and a rocprofv3 kernel-trace summary of the default bench.
 # usage (on the box): bash tools/round_check.sh <tag>
 set -u
 tag=${1:-rx}
@@ -16,12 +16,7 @@ tail -1 "$O/smoke.log"
 timeout -k 10 300 python bench.py > "$O/bench_c1.json" 2> "$O/bench_c1.err" \
   || { echo "bench failed"; tail -20 "$O/bench_c1.err"; exit 1; }
 cat "$O/bench_c1.json"
-for c in c2 c3; do
-  timeout -k 10 200 python bench.py --config $c --no-cpu > "$O/bench_$c.json" 2> "$O/bench_$c.err" \
-    || { echo "bench $c failed"; tail -20 "$O/bench_$c.err"; exit 1; }
-  cat "$O/bench_$c.json"
-done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/prof" -o run -- python3 bench.py --no-cpu > "$O/prof.log" 2>&1 \
   || { echo "rocprof failed"; tail -20 "$O/prof.log"; exit 1; }
-find "$O/prof" -name '*kernel_stats.csv' | head -1 | xargs -I{} cp {} "$O/kernel_stats.csv"
+cp "$(find "$O/prof" -name '*kernel_stats.csv' -print -quit)" "$O/kernel_stats.csv"
 echo done
