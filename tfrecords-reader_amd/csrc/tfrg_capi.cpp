@@ -131,7 +131,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
   // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
   // 32 round shifts x^(8192 * 2^k)
-  std::vector<uint32_t> tab(8192), cst(128);
+  std::vector<uint32_t> tab(8192 + 16384), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -140,6 +140,10 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   memcpy(tab.data() + 1024, M, 4096);
   memcpy(tab.data() + 2048, T.t, 8192);
   memcpy(tab.data() + 4096, T.t, 16384);  // slice-by-16 (streaming CRC)
+  // the slice-by-16 tables in the streaming CRC's bank-conflict-free layout (tfrg_kernels.hip
+  // chunk_rot): row e of 64 dwords, column c < 47 holding table (c + 1) & 15
+  for (int e = 0; e < 256; ++e)
+    for (int col = 0; col < 47; ++col) tab[8192 + e * 64 + col] = T.t[(col + 1) & 15][e];
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts

@@ -1697,25 +1697,25 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
 
 // Exact reference walk (decoder.pyx:107-300 in its own level-by-level error precedence), one lane per
 // record of the slow list, reading the record from HBM; also the framing errors and schema misses.
-template <int R, bool COMPAT, bool GORD>
+template <int R, bool COMPAT, bool GORD, uint32_t BLK>
 __device__ void role_slow_count(const DevBatch& B, const DevSchema& sc, const DevOut& o,
                                 const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t nslow = o.info[kInfoSlow];
-  if (blockIdx.x * kLaneBlock >= nslow) return;  // block-uniform
+  if (blockIdx.x * BLK >= nslow) return;  // block-uniform
   uint32_t* tab = lds;                            // 2048 * R dwords (slice-by-8 set; step4 uses 0..3)
   uint32_t* cnt = lds + 2048 * R;
   const uint32_t S = sc.n_slots;
-  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + (GORD ? 0u : S * kLaneBlock));
-  for (uint32_t i = threadIdx.x; i < 2048u * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + (GORD ? 0u : S * BLK));
+  for (uint32_t i = threadIdx.x; i < 2048u * R; i += BLK) tab[i] = crc_tab[2048 + i / R];
   __syncthreads();
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
-  for (uint32_t i = blockIdx.x * kLaneBlock + threadIdx.x; i < nslow; i += gridDim.x * kLaneBlock) {
+  for (uint32_t i = blockIdx.x * BLK + threadIdx.x; i < nslow; i += gridDim.x * BLK) {
     const uint32_t r = o.slow_list[i];
     RecView v = rec_view(B, r);
     int64_t aux = 0;
     CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
-                           GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
+                           GORD ? B.n : (uint32_t)BLK, 0, B.n, r, v.p0, false, true};
     if constexpr (!GORD) sink.cnt = (lds_u32*)(cnt + threadIdx.x);
     int status = v.status;
     if (status == TFRG_OK) {
@@ -1806,7 +1806,8 @@ constexpr uint32_t kNumCst = 128;
 
 // U(0, 16-byte chunk at q) of the payload [a, b): bytes outside zeroed, the first 4 payload bytes
 // inverted (the ~0 initial state)
-__device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uint64_t b, const LdsTab<1>& T) {
+template <class TabT>
+__device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uint64_t b, const TabT& T) {
   uint32_t ws[4] = {w.x, w.y, w.z, w.w};
   if (q < a + 4 || q + 16 > b) {
     // chunk-relative byte bounds in [0, 16]: keep [lo, hi), invert [lo, li) (the payload's first 4)
@@ -1836,6 +1837,27 @@ __device__ __forceinline__ uint32_t chunk_u(uint4 w, uint64_t q, uint64_t a, uin
     r1 ^= T.at4(13 - 4 * k2, byte_x4<2>(x)) ^ T.at4(12 - 4 * k2, byte_x4<3>(x));
   }
   return r0 ^ r1;
+}
+
+// The masking of chunk_u alone: bytes outside the payload [a, b) zeroed, its first 4 bytes inverted.
+__device__ __forceinline__ uint4 chunk_mask(uint4 w, uint64_t q, uint64_t a, uint64_t b) {
+  uint32_t ws[4] = {w.x, w.y, w.z, w.w};
+  const int64_t la = (int64_t)(a - q), lb = (int64_t)(b - q);
+  const uint32_t lo = la <= 0 ? 0u : (la >= 16 ? 16u : (uint32_t)la);
+  const uint32_t hi = lb <= 0 ? 0u : (lb >= 16 ? 16u : (uint32_t)lb);
+  const uint32_t li = la + 4 <= 0 ? 0u : (la + 4 >= 16 ? 16u : (uint32_t)(la + 4));
+#pragma unroll
+  for (int k2 = 0; k2 < 4; ++k2) {
+    auto upto = [](uint32_t x, int k) {
+      const uint32_t n = x <= 4u * k ? 0u : (x - 4u * k >= 4u ? 4u : x - 4u * k);
+      return n >= 4u ? 0xffffffffu : (1u << (8u * n)) - 1u;
+    };
+    const uint32_t below_lo = upto(lo, k2);
+    const uint32_t keep = upto(hi, k2) & ~below_lo;
+    const uint32_t inv = upto(li, k2) & ~below_lo & keep;
+    ws[k2] = (ws[k2] & keep) ^ inv;
+  }
+  return make_uint4(ws[0], ws[1], ws[2], ws[3]);
 }
 
 // chunk_u of an interior chunk (no masks) with the slice-by-16 tables at LDS address 0: all 16
@@ -1878,21 +1900,96 @@ __device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
               xor3(r[9], r[10], r[11]), xor3(r[12], r[13], r[14])) ^ r[15];
 }
 
+// Bank-conflict-free slice-by-16 (the streaming CRC's LDS layout): the 16 tables are laid out in
+// rows of 64 dwords, row e = entry e, column c holding T[(c + 1) & 15][e] (c < 47). Lane l reads its
+// chunk ROTATED by rho = l & 15 bytes: at instruction t its byte t is chunk byte (t + rho) & 15, whose
+// table 15 - ((t + rho) & 15) sits in column 15 - rho + 16 h + 15 - t, h = (l >> 4) & 1. The bank
+// ((a / 4) mod 32) is then 15 - rho + 16 h + 15 - t mod 32: the 32 lanes of a ds_read_b32 group hit 32
+// different banks whatever the data (random-byte lookups into one shared table conflicted ~3x,
+// profiles/r02/pmc_c2_k_tail_count.json). The address (e << 8) | lane base is ONE v_perm_b32; the
+// table base and the column's t part are the instruction's immediate offset.
+constexpr uint32_t kRotTabOff = 4096;  // byte offset of the rotated table in LDS (after A1)
+struct CrcRot {
+  uint64_t m1, m2;  // lanes whose rho has bit 2 / bit 3 set (dword rotation by 1 / 2)
+  uint32_t s;       // rho & 3 (byte funnel)
+  uint32_t basel;   // 4 * (15 - rho + 16 h)
+};
+__device__ __forceinline__ CrcRot crc_rot_init(uint32_t lane) {
+  const uint32_t rho = lane & 15u;
+  CrcRot r;
+  r.m1 = __ballot((rho >> 2) & 1u);
+  r.m2 = __ballot((rho >> 3) & 1u);
+  r.s = rho & 3u;
+  r.basel = 4u * (15u - rho + 16u * ((lane >> 4) & 1u));
+  return r;
+}
+__device__ __forceinline__ uint32_t crc_perm(uint32_t x, uint32_t basel, uint32_t sel) {
+  return __builtin_amdgcn_perm(x, basel, sel);
+}
+__device__ __forceinline__ uint32_t chunk_rot(uint4 w, const CrcRot& R, uint32_t lane) {
+  const uint64_t bit = 1ull << lane;
+  const bool b2 = (R.m2 & bit) != 0, b1 = (R.m1 & bit) != 0;
+  // dword rotation by q = rho >> 2: E[i] = D[(i + q) & 3]
+  uint32_t e0 = b2 ? w.z : w.x, e1 = b2 ? w.w : w.y, e2 = b2 ? w.x : w.z, e3 = b2 ? w.y : w.w;
+  const uint32_t f0 = b1 ? e1 : e0, f1 = b1 ? e2 : e1, f2 = b1 ? e3 : e2, f3 = b1 ? e0 : e3;
+  // byte funnel by rho & 3: R[i] = bytes (4i + rho ..) of the chunk
+  const uint32_t r0 = __builtin_amdgcn_alignbyte(f1, f0, R.s), r1 = __builtin_amdgcn_alignbyte(f2, f1, R.s);
+  const uint32_t r2 = __builtin_amdgcn_alignbyte(f3, f2, R.s), r3 = __builtin_amdgcn_alignbyte(f0, f3, R.s);
+  // v_perm selectors: byte 0 from the lane base (src1 byte 0), byte 1 = byte k of x (src0), rest 0
+  constexpr uint32_t S0 = 0x0c0c0400u, S1 = 0x0c0c0500u, S2 = 0x0c0c0600u, S3 = 0x0c0c0700u;
+  const uint32_t bl = R.basel;
+  uint32_t v[16];
+  v[0] = crc_perm(r0, bl, S0); v[1] = crc_perm(r0, bl, S1); v[2] = crc_perm(r0, bl, S2); v[3] = crc_perm(r0, bl, S3);
+  v[4] = crc_perm(r1, bl, S0); v[5] = crc_perm(r1, bl, S1); v[6] = crc_perm(r1, bl, S2); v[7] = crc_perm(r1, bl, S3);
+  v[8] = crc_perm(r2, bl, S0); v[9] = crc_perm(r2, bl, S1); v[10] = crc_perm(r2, bl, S2); v[11] = crc_perm(r2, bl, S3);
+  v[12] = crc_perm(r3, bl, S0); v[13] = crc_perm(r3, bl, S1); v[14] = crc_perm(r3, bl, S2); v[15] = crc_perm(r3, bl, S3);
+  // all 16 reads issued before the one wait; instruction t's immediate = table base + 4 (15 - t)
+  asm volatile(
+      "ds_read_b32 %0, %0 offset:4156\n\t"
+      "ds_read_b32 %1, %1 offset:4152\n\t"
+      "ds_read_b32 %2, %2 offset:4148\n\t"
+      "ds_read_b32 %3, %3 offset:4144\n\t"
+      "ds_read_b32 %4, %4 offset:4140\n\t"
+      "ds_read_b32 %5, %5 offset:4136\n\t"
+      "ds_read_b32 %6, %6 offset:4132\n\t"
+      "ds_read_b32 %7, %7 offset:4128\n\t"
+      "ds_read_b32 %8, %8 offset:4124\n\t"
+      "ds_read_b32 %9, %9 offset:4120\n\t"
+      "ds_read_b32 %10, %10 offset:4116\n\t"
+      "ds_read_b32 %11, %11 offset:4112\n\t"
+      "ds_read_b32 %12, %12 offset:4108\n\t"
+      "ds_read_b32 %13, %13 offset:4104\n\t"
+      "ds_read_b32 %14, %14 offset:4100\n\t"
+      "ds_read_b32 %15, %15 offset:4096\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
+        "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15]));
+  return xor3(xor3(xor3(v[0], v[1], v[2]), xor3(v[3], v[4], v[5]), xor3(v[6], v[7], v[8])),
+              xor3(v[9], v[10], v[11]), xor3(v[12], v[13], v[14])) ^ v[15];
+}
+// table j's entry at byte offset bx4 = 4 * index, read from the rotated layout (masked edge chunks)
+struct RotTabView {
+  const uint8_t* l;  // LDS base
+  __device__ __forceinline__ uint32_t at4(uint32_t j, uint32_t bx4) const {
+    return *reinterpret_cast<const uint32_t*>(l + kRotTabOff + (bx4 << 6) + 4u * ((j + 15u) & 15u));
+  }
+};
+
 __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
   return M[S & 0xffu] ^ M[256 + ((S >> 8) & 0xffu)] ^ M[512 + ((S >> 16) & 0xffu)] ^ M[768 + (S >> 24)];
 }
 
-// mul_tab of the x^8192 table A1 at LDS byte 16384 (after the slice-by-16 tables at 0), with SDWA
+// mul_tab of the x^8192 table A1 at LDS byte 0 (before the rotated slice-by-16 table), with SDWA
 // byte offsets and immediate table offsets: 4 VALU + 4 LDS reads + 2 XOR
 __device__ __forceinline__ uint32_t mul_a1_lds(uint32_t S) {
   uint32_t m0, m1, m2, m3;
   const uint32_t two = 2u;
   asm volatile(
       TFRG_SDWA(0, 4, 5, 0) TFRG_SDWA(1, 4, 5, 1) TFRG_SDWA(2, 4, 5, 2) TFRG_SDWA(3, 4, 5, 3)
-      "ds_read_b32 %0, %0 offset:16384\n\t"
-      "ds_read_b32 %1, %1 offset:17408\n\t"
-      "ds_read_b32 %2, %2 offset:18432\n\t"
-      "ds_read_b32 %3, %3 offset:19456\n\t"
+      "ds_read_b32 %0, %0\n\t"
+      "ds_read_b32 %1, %1 offset:1024\n\t"
+      "ds_read_b32 %2, %2 offset:2048\n\t"
+      "ds_read_b32 %3, %3 offset:3072\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)
       : "v"(two), "v"(S));
@@ -2022,6 +2119,7 @@ __device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, co
   }
 }
 
+template <uint32_t BLK>
 __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut& o, const uint32_t* __restrict__ crc_tab,
                                 const uint32_t* __restrict__ consts, uint32_t n_slots) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
@@ -2030,17 +2128,22 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   const uint32_t nrec = (uint32_t)(ctr >> kCrcIdxShift);
   const uint64_t TR = ctr & kCrcRoundMask;
   if (!nrec) return;  // (grid-uniform)
-  uint32_t* tab = lds;         // [16][256] slice-by-16
-  uint32_t* A1 = lds + 4096;   // [4][256] (x) x^8192
-  uint32_t* cst = lds + 5120;  // [kNumCst]
-  for (uint32_t i = threadIdx.x; i < 4096u; i += kLaneBlock) tab[i] = crc_tab[4096 + i];
-  for (uint32_t i = threadIdx.x; i < 1024u; i += kLaneBlock) A1[i] = crc_tab[1024 + i];
-  for (uint32_t i = threadIdx.x; i < kNumCst; i += kLaneBlock) cst[i] = consts[i];
+  uint32_t* A1 = lds;           // [4][256] (x) x^8192
+  uint32_t* rot = lds + 1024;   // [256][64] rotated slice-by-16 (chunk_rot)
+  uint32_t* cst = lds + 17408;  // [kNumCst]
+  for (uint32_t i = threadIdx.x; i < 1024u; i += BLK) A1[i] = crc_tab[1024 + i];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(crc_tab + 8192);
+    uint4* dst = reinterpret_cast<uint4*>(rot);
+    for (uint32_t i = threadIdx.x; i < 4096u; i += BLK) dst[i] = src[i];
+  }
+  for (uint32_t i = threadIdx.x; i < kNumCst; i += BLK) cst[i] = consts[i];
   __syncthreads();
-  const LdsTab<1> T{tab, 0};
-  const bool tab_at0 = (uint32_t)(uintptr_t)tab == 0u;  // (the asm chunk path addresses LDS 0)
+  const RotTabView T{reinterpret_cast<const uint8_t*>(lds)};
+  const bool tab_at0 = (uint32_t)(uintptr_t)lds == 0u;  // (the asm chunk path addresses LDS 0)
   const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
-  const uint64_t W = (uint64_t)gridDim.x * (kLaneBlock / 64), wv = (uint64_t)blockIdx.x * (kLaneBlock / 64) + wib;
+  const CrcRot RR = crc_rot_init(lane);
+  const uint64_t W = (uint64_t)gridDim.x * (BLK / 64), wv = (uint64_t)blockIdx.x * (BLK / 64) + wib;
   const uint64_t R0 = TR * wv / W, R1 = TR * (wv + 1) / W;
   if (R0 >= R1) return;  // (wave-uniform; no barrier follows)
   PHASE_MARK(q0);
@@ -2075,6 +2178,22 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     g.r0 = Rs;
     g.n = Rs < lim ? (uint32_t)(lim - Rs < (uint64_t)kCrcDepth ? lim - Rs : (uint64_t)kCrcDepth) : 0u;
     if (!g.n) return;
+    const uint64_t rl = Rs + g.n - 1u;
+    const uint32_t k0 = (uint32_t)__popcll(__ballot(w.base <= Rs)) - 1u;
+    const uint32_t kl = (uint32_t)__popcll(__ballot(w.base <= rl)) - 1u;
+    if (k0 == kl) {  // (scalar) the whole group inside one record: its entry once
+      const CrcEnt e = crc_ent(w, k0);
+      const uint64_t ch0 = e.E + 64ull * Rs - lane;
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
+        const uint32_t dd = (uint32_t)d < g.n ? (uint32_t)d : g.n - 1u;
+        g.rd[d] = Rs + dd;
+        g.kd[d] = k0;
+        const uint64_t ch = ch0 + 64ull * dd;
+        g.wd[d] = *reinterpret_cast<const uint4*>(B.bytes + (((int64_t)ch >= (int64_t)e.c0 ? ch : e.c0) << 4));
+      }
+      return;
+    }
 #pragma unroll
     for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
       g.rd[d] = Rs + ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u);
@@ -2100,10 +2219,22 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     }
     if (!edge && tab_at0) {  // interior group: one LDS round trip per chunk
 #pragma unroll
-      for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_u16_lds0(g.wd[d]);
+      for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_rot(g.wd[d], RR, lane);
     } else if (!edge) {
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);
+    } else if (tab_at0) {  // edge rounds: masked chunks, the same conflict-free lookups
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) {
+        const CrcEnt e = crc_ent(w, g.kd[d]);
+        uint4 x = g.wd[d];
+        if (g.rd[d] <= e.bas + 1u || g.rd[d] == e.bas + e.J - 1u) {
+          const uint64_t ch = e.E + 64ull * g.rd[d] - lane;
+          const uint64_t a = rl64(w.a, g.kd[d]), b = rl64(w.b, g.kd[d]);
+          x = (int64_t)ch >= (int64_t)e.c0 ? chunk_mask(x, ch << 4, a, b) : make_uint4(0, 0, 0, 0);
+        }
+        rc[d] = chunk_rot(x, RR, lane);
+      }
     } else {
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) {
@@ -2129,7 +2260,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
           next = (int)g.kd[d];
           continue;
         }
-        S = mul_tab(A1, S) ^ rc[d];
+        S = (tab_at0 ? mul_a1_lds(S) : mul_tab(A1, S)) ^ rc[d];
       }
       if (stop == g.n) break;
       if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
@@ -2175,13 +2306,15 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
 // lists only records it accepted), so a strict CRC rejection of role 2 never meets role 1's records.
 // (Role 2 as its own kernel at 5 instead of 4 waves per SIMD measured the same on C2: 0.129 vs 0.130
 // ms; its own launch cost every batch ~6.5 us.)
+// 512-thread blocks: the streaming CRC's 70 KiB of LDS tables then still leave 4 waves per SIMD.
+constexpr uint32_t kTailBlock = 512;
 template <bool COMPAT, bool GORD>
-__global__ __launch_bounds__(kLaneBlock, 4) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kTailBlock, 2) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            const uint32_t* __restrict__ consts, uint32_t lane_max) {
-  role_slow_count<1, COMPAT, GORD>(B, sc, o, crc_tab, lane_max);
+  role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);
   __syncthreads();  // (the LDS tables are reloaded by role 2)
-  role_crc_stream(B, o, crc_tab, consts, sc.n_slots);
+  role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots);
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in
@@ -3002,7 +3135,6 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // speculative placement only with the per-lane LDS dict (MODE 0); the later kernels see the same
   DevSchema scx = sc;
   if (lane_lds > kLaneLdsBudget || !fast_ok) scx.spec = nullptr;
-  const size_t slow_lds = 2048ull * 4 + dict_lane;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
 
   mark(kStageLaneCount);
@@ -3033,16 +3165,21 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
   // the large payloads evenly over the waves; role 1 grid-strides over the slow list)
   {
-    const bool gord = slow_lds > kLaneLdsBudget;
-    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_lds, (5120 + kNumCst) * 4);
+    // (role 1's per-lane dicts for kTailBlock threads, else its global-dict form)
+    const size_t slow_tail = 2048ull * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2);
+    const bool gord = slow_tail > kLaneLdsBudget;
+    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (17408 + kNumCst) * 4);
     const void* fn = gord ? reinterpret_cast<const void*>(&k_tail_count<COMPAT, true>)
                           : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
-    const uint32_t g = (uint32_t)resident_grid(fn, lds, false);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTailBlock, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const uint32_t g = (uint32_t)(per_cu * cfg.num_cus);
     if (gord)
-      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kLaneBlock), lds, st, b, scx, o, d_tab, d_consts,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, o, d_tab, d_consts,
                          cfg.lane_max);
     else
-      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kLaneBlock), lds, st, b, scx, o, d_tab,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, o, d_tab,
                          d_consts, cfg.lane_max);
   }
   mark(kStageSpine);
