@@ -131,7 +131,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
   // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
   // 32 round shifts x^(8192 * 2^k)
-  std::vector<uint32_t> tab(8192 + 16384), cst(128);
+  std::vector<uint32_t> tab(8192 + 16384 + 2048), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -144,6 +144,11 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   // chunk_rot): row e of 64 dwords, column c < 47 holding table (c + 1) & 15
   for (int e = 0; e < 256; ++e)
     for (int col = 0; col < 47; ++col) tab[8192 + e * 64 + col] = T.t[(col + 1) & 15][e];
+  // multiply-by-x^16384 and x^32768 tables (the streaming CRC's split Horner sum over 4 rounds)
+  crc_make_mul_tables(gf_xpow8(2048), M);
+  memcpy(tab.data() + 24576, M, 4096);
+  crc_make_mul_tables(gf_xpow8(4096), M);
+  memcpy(tab.data() + 25600, M, 4096);
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts

@@ -1908,7 +1908,7 @@ __device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
 // different banks whatever the data (random-byte lookups into one shared table conflicted ~3x,
 // profiles/r02/pmc_c2_k_tail_count.json). The address (e << 8) | lane base is ONE v_perm_b32; the
 // table base and the column's t part are the instruction's immediate offset.
-constexpr uint32_t kRotTabOff = 4096;  // byte offset of the rotated table in LDS (after A1)
+constexpr uint32_t kRotTabOff = 12288;  // byte offset of the rotated table in LDS (after A1, A2, A4)
 struct CrcRot {
   uint64_t m1, m2;  // lanes whose rho has bit 2 / bit 3 set (dword rotation by 1 / 2)
   uint32_t s;       // rho & 3 (byte funnel)
@@ -1945,22 +1945,22 @@ __device__ __forceinline__ uint32_t chunk_rot(uint4 w, const CrcRot& R, uint32_t
   v[12] = crc_perm(r3, bl, S0); v[13] = crc_perm(r3, bl, S1); v[14] = crc_perm(r3, bl, S2); v[15] = crc_perm(r3, bl, S3);
   // all 16 reads issued before the one wait; instruction t's immediate = table base + 4 (15 - t)
   asm volatile(
-      "ds_read_b32 %0, %0 offset:4156\n\t"
-      "ds_read_b32 %1, %1 offset:4152\n\t"
-      "ds_read_b32 %2, %2 offset:4148\n\t"
-      "ds_read_b32 %3, %3 offset:4144\n\t"
-      "ds_read_b32 %4, %4 offset:4140\n\t"
-      "ds_read_b32 %5, %5 offset:4136\n\t"
-      "ds_read_b32 %6, %6 offset:4132\n\t"
-      "ds_read_b32 %7, %7 offset:4128\n\t"
-      "ds_read_b32 %8, %8 offset:4124\n\t"
-      "ds_read_b32 %9, %9 offset:4120\n\t"
-      "ds_read_b32 %10, %10 offset:4116\n\t"
-      "ds_read_b32 %11, %11 offset:4112\n\t"
-      "ds_read_b32 %12, %12 offset:4108\n\t"
-      "ds_read_b32 %13, %13 offset:4104\n\t"
-      "ds_read_b32 %14, %14 offset:4100\n\t"
-      "ds_read_b32 %15, %15 offset:4096\n\t"
+      "ds_read_b32 %0, %0 offset:12348\n\t"
+      "ds_read_b32 %1, %1 offset:12344\n\t"
+      "ds_read_b32 %2, %2 offset:12340\n\t"
+      "ds_read_b32 %3, %3 offset:12336\n\t"
+      "ds_read_b32 %4, %4 offset:12332\n\t"
+      "ds_read_b32 %5, %5 offset:12328\n\t"
+      "ds_read_b32 %6, %6 offset:12324\n\t"
+      "ds_read_b32 %7, %7 offset:12320\n\t"
+      "ds_read_b32 %8, %8 offset:12316\n\t"
+      "ds_read_b32 %9, %9 offset:12312\n\t"
+      "ds_read_b32 %10, %10 offset:12308\n\t"
+      "ds_read_b32 %11, %11 offset:12304\n\t"
+      "ds_read_b32 %12, %12 offset:12300\n\t"
+      "ds_read_b32 %13, %13 offset:12296\n\t"
+      "ds_read_b32 %14, %14 offset:12292\n\t"
+      "ds_read_b32 %15, %15 offset:12288\n\t"
       "s_waitcnt lgkmcnt(0)"
       : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]),
         "+v"(v[8]), "+v"(v[9]), "+v"(v[10]), "+v"(v[11]), "+v"(v[12]), "+v"(v[13]), "+v"(v[14]), "+v"(v[15]));
@@ -1981,6 +1981,25 @@ __device__ __forceinline__ uint32_t mul_tab(const uint32_t* M, uint32_t S) {
 
 // mul_tab of the x^8192 table A1 at LDS byte 0 (before the rotated slice-by-16 table), with SDWA
 // byte offsets and immediate table offsets: 4 VALU + 4 LDS reads + 2 XOR
+#define TFRG_MUL_LDS(NAME, O0, O1, O2, O3)                                                        \
+  __device__ __forceinline__ uint32_t NAME(uint32_t S) {                                          \
+    uint32_t m0, m1, m2, m3;                                                                      \
+    const uint32_t two = 2u;                                                                      \
+    asm volatile(TFRG_SDWA(0, 4, 5, 0) TFRG_SDWA(1, 4, 5, 1) TFRG_SDWA(2, 4, 5, 2) TFRG_SDWA(3, 4, 5, 3) \
+                 "ds_read_b32 %0, %0 offset:" #O0 "\n\t"                                        \
+                 "ds_read_b32 %1, %1 offset:" #O1 "\n\t"                                        \
+                 "ds_read_b32 %2, %2 offset:" #O2 "\n\t"                                        \
+                 "ds_read_b32 %3, %3 offset:" #O3 "\n\t"                                        \
+                 "s_waitcnt lgkmcnt(0)"                                                           \
+                 : "=&v"(m0), "=&v"(m1), "=&v"(m2), "=&v"(m3)                                     \
+                 : "v"(two), "v"(S));                                                             \
+    return xor3(m0, m1, m2) ^ m3;                                                                 \
+  }
+// (x) x^16384 and x^32768 at LDS bytes 4096 and 8192: a group of 4 rounds of one record is summed as
+// S A^4 + (rc0 A + rc1) A^2 + (rc2 A + rc3): two dependent LDS round trips instead of four
+TFRG_MUL_LDS(mul_a2_lds, 4096, 5120, 6144, 7168)
+TFRG_MUL_LDS(mul_a4_lds, 8192, 9216, 10240, 11264)
+
 __device__ __forceinline__ uint32_t mul_a1_lds(uint32_t S) {
   uint32_t m0, m1, m2, m3;
   const uint32_t two = 2u;
@@ -2128,10 +2147,11 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   const uint32_t nrec = (uint32_t)(ctr >> kCrcIdxShift);
   const uint64_t TR = ctr & kCrcRoundMask;
   if (!nrec) return;  // (grid-uniform)
-  uint32_t* A1 = lds;           // [4][256] (x) x^8192
-  uint32_t* rot = lds + 1024;   // [256][64] rotated slice-by-16 (chunk_rot)
-  uint32_t* cst = lds + 17408;  // [kNumCst]
+  uint32_t* A1 = lds;           // [4][256] (x) x^8192, then (x) x^16384, (x) x^32768
+  uint32_t* rot = lds + 3072;   // [256][64] rotated slice-by-16 (chunk_rot)
+  uint32_t* cst = lds + 19456;  // [kNumCst]
   for (uint32_t i = threadIdx.x; i < 1024u; i += BLK) A1[i] = crc_tab[1024 + i];
+  for (uint32_t i = threadIdx.x; i < 2048u; i += BLK) A1[1024 + i] = crc_tab[24576 + i];
   {
     const uint4* src = reinterpret_cast<const uint4*>(crc_tab + 8192);
     uint4* dst = reinterpret_cast<uint4*>(rot);
@@ -2212,10 +2232,15 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     // bytes, inverted, may run into the chunk after a's: that chunk opens the second round when the
     // first holds only a's chunk) and its last round
     bool edge = false;
+    if (g.kd[0] == g.kd[kCrcDepth - 1]) {  // (scalar) one record: its first two rounds or its last
+      const uint64_t bas = rl64(w.base, g.kd[0]);
+      edge = g.r0 <= bas + 1u || g.r0 + g.n >= rl64(w.base, g.kd[0] + 1u);
+    } else {
 #pragma unroll
-    for (int d = 0; d < kCrcDepth; ++d) {
-      const uint64_t bas = rl64(w.base, g.kd[d]);
-      edge |= g.rd[d] <= bas + 1u || g.rd[d] == rl64(w.base, g.kd[d] + 1u) - 1u;
+      for (int d = 0; d < kCrcDepth; ++d) {
+        const uint64_t bas = rl64(w.base, g.kd[d]);
+        edge |= g.rd[d] <= bas + 1u || g.rd[d] == rl64(w.base, g.kd[d] + 1u) - 1u;
+      }
     }
     if (!edge && tab_at0) {  // interior group: one LDS round trip per chunk
 #pragma unroll
@@ -2247,6 +2272,12 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
           rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);  // (interior: no masks)
         }
       }
+    }
+    static_assert(kCrcDepth == 4, "the split Horner sum below is spelled out for 4 rounds");
+    if (tab_at0 && g.n == 4u && (int)g.kd[0] == cur && g.kd[3] == g.kd[0]) {  // (scalar) whole group, open record
+      const uint32_t a = mul_a1_lds(rc[0]) ^ rc[1], b = mul_a1_lds(rc[2]) ^ rc[3];
+      S = mul_a4_lds(S) ^ mul_a2_lds(a) ^ b;
+      return;
     }
     // the group one record at a time: a record change ends the pass at `stop` (one flush site)
     for (uint32_t d0 = 0;;) {
@@ -3168,7 +3199,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     // (role 1's per-lane dicts for kTailBlock threads, else its global-dict form)
     const size_t slow_tail = 2048ull * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2);
     const bool gord = slow_tail > kLaneLdsBudget;
-    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (17408 + kNumCst) * 4);
+    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (19456 + kNumCst) * 4);
     const void* fn = gord ? reinterpret_cast<const void*>(&k_tail_count<COMPAT, true>)
                           : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
     int per_cu = 0;
