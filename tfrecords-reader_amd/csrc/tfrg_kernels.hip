@@ -2985,10 +2985,133 @@ __device__ __forceinline__ bool int64_balanced(const FastSrc& fs, const DevOut& 
   return !__ballot(bad);
 }
 
+// One varint whose bytes are stage [s, s + nb), nb in 1..10 (the caller knows where it ends): the
+// reference's compat shifts as varint_bf (decoder.pyx:34-50).
+template <bool COMPAT>
+__device__ __forceinline__ int64_t varint_known(const uint8_t* l, uint32_t s, uint32_t nb) {
+  const uint32_t sh = s & 3u;
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(l) + (s >> 2);
+  const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
+  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+  const uint32_t m0 = bytes_mask(nb), m1 = nb > 4u ? bytes_mask(nb - 4u) : 0u, m2 = nb > 8u ? bytes_mask(nb - 8u) : 0u;
+  const uint32_t x = vgroups(w0, m0), x1 = vgroups(w1, m1), x2 = vgroups(w2, m2);
+  if (COMPAT) {
+    const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
+    const bool neg = ((x1 >> 3) | (x2 >> 7)) & 1u;
+    return (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
+  }
+  return (int64_t)((uint64_t)x | ((uint64_t)x1 << 28) | ((uint64_t)x2 << 56));
+}
+
+// Canonical packed int64 lists of one staged record, value-parallel with COALESCED stores. In
+// int64_balanced every lane decodes its own byte range, so one store instruction scatters 8-byte
+// values over ~64 different lines (the gather's int64 part measured 1.12 of its 1.65 ms). Here
+// pass A walks the stage span of the eligible bodies 256 bytes per step (lane j: aligned dword j),
+// keeps the terminator bytes (< 0x80) inside a body and numbers them across the wave (three
+// ballots + mbcnt), writing each one's stage offset (u16) and slot (u8) into a ring of kRingN in LDS:
+// terminator g ends value g of the axis (the eligible slots in order). Pass B, as soon as 64 ends
+// are pending, gives value gb + j to lane j: its end is ring[g], its start the slot's body start
+// (first value) or ring[g - 1] + 1, the slot's parameters one ds_bpermute each; lanes j and j + 1
+// then store neighbouring values of one slot. Requires the eligible bodies in increasing stage order
+// with the slot index and 32-bit value positions (else -1: the caller takes int64_balanced). Every
+// slot's last value must end on its body's last byte and the terminators must number exactly the
+// counts (else 0: per-lane redo, which rewrites the whole range; stores here never leave
+// [dst, dst + c)).
+constexpr uint32_t kRingN = 324;  // 64 pending + 1 previous end + 256 of one pass-A step (+ pad)
+// per wave in k_tail_gather: stage + ring (3 workgroups of 4 waves per CU, with LDS granularity)
+constexpr uint32_t kWRegion = (kWStageStride + kRingN * 3u + 15u) & ~15u;  // (16-B aligned stages)
+
+template <bool COMPAT>
+__device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bool iv, uint32_t bo, uint32_t bl,
+                                          uint32_t c, uint64_t dst, uint32_t lane, uint16_t* ring) {
+  const uint64_t m = __ballot(iv);
+  if (!m) return 1;
+  uint8_t* ring_k = reinterpret_cast<uint8_t*>(ring + kRingN);  // each entry's slot
+  const uint32_t bs = fs.p + bo, be = bs + bl;  // stage offsets of the body
+  const uint64_t lt = (1ull << lane) - 1ull;
+  {  // physical order = slot order, and 32-bit value positions
+    const uint64_t pm = m & lt;
+    const int pl = pm ? 63 - __builtin_clzll(pm) : (int)lane;
+    const uint32_t pbe = (uint32_t)__shfl((int)be, pl, 64);
+    if (__ballot(iv && ((pm && pbe > bs) || ((dst + c) >> 32) != 0u))) return -1;
+  }
+  const uint32_t n = iv ? c : 0u;
+  const uint32_t incl = wave_incl_scan_u32(n, lane);
+  const uint32_t N = __builtin_amdgcn_readlane(incl, 63);
+  const uint32_t pk_b = bs | (bl << 16), pk_c = (incl - n) | (n << 16), d32 = (uint32_t)dst;
+  const uint32_t k_first = (uint32_t)__builtin_ctzll(m), k_last = 63u - (uint32_t)__builtin_clzll(m);
+  const uint32_t Q0 = __builtin_amdgcn_readlane(bs, k_first) & ~3u, Qend = __builtin_amdgcn_readlane(be, k_last);
+  const uint32_t* L32 = reinterpret_cast<const uint32_t*>(fs.l);
+  uint32_t gtot = 0, rh = 0;  // terminators so far; ring slot of terminator gtot
+  uint32_t gb = 0, rb = 0;    // values decoded so far; ring slot of value gb
+  bool bad = false;
+  auto pass_b = [&](uint32_t avail) {
+    const bool act = lane < avail;
+    uint32_t r = rb + lane;
+    if (r >= kRingN) r -= kRingN;
+    const uint32_t e = ring[r];
+    const uint32_t ep = ring[r ? r - 1u : kRingN - 1u];
+    const int k = (int)(ring_k[r] & 63u);
+    const uint32_t pb = (uint32_t)__shfl((int)pk_b, k, 64), pc = (uint32_t)__shfl((int)pk_c, k, 64);
+    const uint32_t pd = (uint32_t)__shfl((int)d32, k, 64);
+    const uint32_t sbs = pb & 0xffffu, sbe = sbs + (pb >> 16), scn = pc >> 16;
+    const uint32_t vi = gb + lane - (pc & 0xffffu);
+    const uint32_t pe = e & 0xffffu;
+    const uint32_t s = vi ? (ep & 0xffffu) + 1u : sbs;
+    const uint32_t nb = pe + 1u - s;  // (wraps huge when pe < s)
+    const bool ok = act && vi < scn && nb - 1u < 10u && (vi + 1u < scn || pe + 1u == sbe);
+    bad |= act && !ok;
+    const int64_t v = varint_known<COMPAT>(fs.l, ok ? s : 0u, ok ? nb : 1u);
+    const uint64_t at = (uint64_t)pd + vi;
+    if (ok && at < o.cap_i64) o.i64[at] = v;
+    gb += avail;
+    rb += avail;
+    if (rb >= kRingN) rb -= kRingN;
+  };
+  for (uint32_t Qw = Q0; Qw < Qend; Qw += 256u) {
+    const uint32_t Q = Qw + 4u * lane;
+    const uint32_t w = Q < Qend ? L32[Q >> 2] : 0u;
+    uint32_t bm = 0, ks = 0;  // bytes of this dword inside an eligible body (bodies are >= 8 bytes apart)
+    uint64_t mw = __ballot(iv && bs < Qw + 256u && be > Qw);  // bodies overlapping this step
+    while (mw) {
+      const uint32_t k = (uint32_t)__builtin_ctzll(mw);
+      mw &= mw - 1ull;
+      const uint32_t sbs = __builtin_amdgcn_readlane(bs, k), sbe = __builtin_amdgcn_readlane(be, k);
+      const uint32_t lo = sbs > Q ? sbs - Q : 0u, hi = sbe > Q ? sbe - Q : 0u;
+      if (hi > lo && lo < 4u) {
+        bm = bytes_mask(hi) & ~bytes_mask(lo);
+        ks = k;
+      }
+    }
+    uint32_t t = ~w & 0x80808080u & bm;
+    const uint32_t nt = (uint32_t)__popc(t);
+    const uint64_t b0 = __ballot(nt & 1u), b1 = __ballot(nt & 2u), b2 = __ballot(nt & 4u);
+    uint32_t at = rh + (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) + 4u * (uint32_t)__popcll(b2 & lt);
+    const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
+    while (t) {
+      const uint32_t a = at >= kRingN ? at - kRingN : at;
+      ring[a] = (uint16_t)(Q + ((uint32_t)__builtin_ctz(t) >> 3));
+      ring_k[a] = (uint8_t)ks;
+      t &= t - 1u;
+      ++at;
+    }
+    gtot += tot;
+    rh += tot;
+    if (rh >= kRingN) rh -= kRingN;
+    wave_lds_sync();
+    while (gtot - gb >= 64u) pass_b(64u);
+    wave_lds_sync();  // (pass B's reads before the next step's writes)
+  }
+  if (gtot > gb) pass_b(gtot - gb);
+  wave_lds_sync();
+  return (!__ballot(bad) && gtot == N) ? 1 : 0;
+}
+
 template <bool COMPAT>
 __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevOut& o, bool present, uint32_t kind,
                                                    uint2 lc, uint32_t cnt, uint64_t dst, uint64_t lo16,
-                                                   uint32_t lane) {
+                                                   uint32_t lane, uint16_t* ring) {
   PHASE_MARK(g0);
   // every lane reads its own slot's chunk header up front: the wave loops below only readlane them
   uint32_t bo = 0, bl = 0;
@@ -3011,7 +3134,12 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   // canonical packed int64 lists: balanced over the whole wave
   const bool iv = packed && kind == TFRG_KIND_INT64 && bl > 0u && fs.l[fs.p + bo + bl - 1u] < 0x80u;
   fail |= packed && kind == TFRG_KIND_INT64 && !iv;
-  if (!int64_balanced<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane)) fail |= iv;
+#ifndef TFRG_INT64_RING
+#define TFRG_INT64_RING 1
+#endif
+  int rr = TFRG_INT64_RING ? int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring) : -1;
+  if (rr < 0) rr = int64_balanced<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane) ? 1 : 0;
+  if (!rr) fail |= iv;
   PHASE_MARK(g1);
   PHASE_ADD(11, gf, g1);
   if (present && (kind == TFRG_KIND_BYTES || fail)) {
@@ -3034,7 +3162,8 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
 #define TFRG_GATHER_PREF 1
 #endif
 template <bool COMPAT>
-__device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage) {
+__device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage,
+                                  uint16_t* ring) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nbig = o.info[kInfoBig];
   if (blockIdx.x * kWavesPerBlock + wib >= nbig) return;  // wave-uniform: no records for this wave
@@ -3097,7 +3226,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     PHASE_MARK(t1);
     PHASE_ADD(9, t0, t1);
     const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-    stage_gather_group<COMPAT>(fs, o, present, kind, lc, c, dst, lo16, lane);
+    stage_gather_group<COMPAT>(fs, o, present, kind, lc, c, dst, lo16, lane, ring);
     for (uint32_t kb = 64; kb < sc.n_slots; kb += 64) {  // wide schemas: further groups of 64 slots
       const uint32_t k = kb + lane;
       bool pk = false;
@@ -3112,7 +3241,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
         dk = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
         kk = sc.slot_kind[k];
       }
-      stage_gather_group<COMPAT>(fs, o, pk, kk, lk, ck, dk, lo16, lane);
+      stage_gather_group<COMPAT>(fs, o, pk, kk, lk, ck, dk, lo16, lane, ring);
     }
     wave_lds_sync();
     PHASE_MARK(t2);
@@ -3127,11 +3256,12 @@ template <bool COMPAT>
 __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWStageStride;
+  uint8_t* stage = reinterpret_cast<uint8_t*>(lds) + wib * kWRegion;
+  uint16_t* ring = reinterpret_cast<uint16_t*>(stage + kWStageStride);  // (int64_ring)
   if (blockIdx.x == 0)  // (read by k_down_gather, which has finished: zero for the next decode)
     for (uint32_t k = threadIdx.x; k < sc.n_slots; k += kWaveBlock) o.irr[k] = 0u;
   role_list_gather<COMPAT>(B, sc, o, lane_max, stage);
-  role_stage_gather<COMPAT>(B, sc, o, stage);
+  role_stage_gather<COMPAT>(B, sc, o, stage, ring);
   role_wave_gather<COMPAT>(B, sc, o);
 }
 
@@ -3228,7 +3358,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   }
   mark(kStageTailGather);
   if (S > 0) {  // the gathers after the scan: lane records' lists, staged and huge large records
-    const size_t lds = (size_t)kWStageStride * kWavesPerBlock;
+    const size_t lds = (size_t)kWRegion * kWavesPerBlock;
     const void* fn = reinterpret_cast<const void*>(&k_tail_gather<COMPAT>);
     int per_cu = 0;  // one round of resident workgroups (3 per CU: a second round would run at 1/3)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
