@@ -3118,15 +3118,30 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   const bool packed = present && kind != TFRG_KIND_BYTES && hdr_0a_v(fs, lc.x, lc.y, bo, bl) &&
                       (kind != TFRG_KIND_FLOAT || !(bl & 3u));
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
-  // canonical float lists: lane j moves value j (contiguous 4-byte stores)
+  // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
+  // that four LDS reads are in flight before the stores
+  constexpr int kFG = 4;
   uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
   while (m) {
-    const int k = __builtin_ctzll(m);
-    m &= m - 1;
-    const uint32_t b0 = __builtin_amdgcn_readlane(bo, k), nf = __builtin_amdgcn_readlane(bl, k) >> 2;
-    const uint64_t d = readlane_u64(dst, k);
-    for (uint32_t j = lane; j < nf; j += 64) {
-      if (d + j < o.cap_f32) o.f32[d + j] = lds_u32u(fs.l, fs.p + b0 + 4u * j);
+    uint32_t fb[kFG], fn[kFG];
+    uint64_t fd[kFG];
+    uint32_t nm = 0;
+#pragma unroll
+    for (int i = 0; i < kFG; ++i) {
+      const int k = m ? __builtin_ctzll(m) : 0;
+      fn[i] = m ? __builtin_amdgcn_readlane(bl, k) >> 2 : 0u;
+      fb[i] = fs.p + __builtin_amdgcn_readlane(bo, k);
+      fd[i] = readlane_u64(dst, k);
+      nm = nm > fn[i] ? nm : fn[i];
+      m &= m - 1;
+    }
+    for (uint32_t j = lane; j < nm; j += 64) {
+      uint32_t x[kFG];
+#pragma unroll
+      for (int i = 0; i < kFG; ++i) x[i] = lds_u32u(fs.l, fb[i] + 4u * (j < fn[i] ? j : 0u));
+#pragma unroll
+      for (int i = 0; i < kFG; ++i)
+        if (j < fn[i] && fd[i] + j < o.cap_f32) o.f32[fd[i] + j] = x[i];
     }
   }
   PHASE_MARK(gf);
@@ -3182,6 +3197,25 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
   q.e2v = B.end[vgpr_launder(q.r2)];
   q.t2v = o.status[vgpr_launder(q.r2)];
   q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
+  // per-slot constants, and the slot metadata of the NEXT record loaded one record ahead (its
+  // latency then hides behind this record's gather instead of opening every record)
+  const bool sl = lane < sc.n_slots;
+  const uint32_t kind_l = sl ? (uint32_t)sc.slot_kind[lane] : 0u;
+  const uint64_t sbase_l = sl ? o.slot_base[lane] : 0ull;
+  uint32_t c_n = 0, rs_n = 0;
+  uint2 lc_n = make_uint2(0, 0);
+  auto meta_load = [&](uint32_t rr, bool okr) {
+    c_n = 0;
+    rs_n = 0;
+    lc_n = make_uint2(0, 0);
+    if (okr && sl) {
+      const size_t at = (size_t)lane * B.n + rr;
+      c_n = o.count[at];
+      lc_n = o.loc[at];
+      rs_n = o.rs[(size_t)lane * (B.n + 1) + rr];
+    }
+  };
+  meta_load(q.r1, q.t1 == TFRG_OK);
   for (; i < nbig; i += stride) {
     PHASE_MARK(t0);
     const uint32_t r = q.r1;
@@ -3197,19 +3231,11 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     }
 #endif
     wave_lds_sync();
-    // slot metadata of this record (issued ahead of the next record's byte loads)
-    bool present = false;
-    uint32_t kind = 0, c = 0;
-    uint2 lc = make_uint2(0, 0);
-    uint64_t dst = 0;
-    if (ok && lane < sc.n_slots) {
-      const size_t at = (size_t)lane * B.n + r;
-      c = o.count[at];
-      present = c && !(c & kCountInline);  // inline single values are k_down_gather's
-      lc = o.loc[at];
-      dst = o.slot_base[lane] + o.rs[(size_t)lane * (B.n + 1) + r];
-      kind = sc.slot_kind[lane];
-    }
+    // slot metadata of this record (loaded during the previous one)
+    const uint32_t c = c_n, kind = kind_l;
+    const uint2 lc = lc_n;
+    const uint64_t dst = sbase_l + rs_n;
+    const bool present = c && !(c & kCountInline);  // inline single values are k_down_gather's
     q.r1 = q.r2;
     q.s1 = rfl64(q.s2v);
     q.e1 = rfl64(q.e2v);
@@ -3222,6 +3248,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     q.s2v = B.start[vgpr_launder(q.r2)];
     q.e2v = B.end[vgpr_launder(q.r2)];
     q.t2v = o.status[vgpr_launder(q.r2)];
+    meta_load(q.r1, q.t1 == TFRG_OK);
     if (!ok) continue;  // wave-uniform
     PHASE_MARK(t1);
     PHASE_ADD(9, t0, t1);
