@@ -292,6 +292,45 @@ def test_long_int64_lists_vs_oracle(dec, orc):
     assert not bad, bad[:10]
 
 
+def test_int64_ring_paths_vs_oracle(dec, orc):
+    """The value-parallel int64 gather (int64_ring) and its fallbacks on staged large records: keys
+    in a per-record shuffled order (bodies out of slot order -> int64_balanced), 1-byte-varint runs
+    (256 terminators in one 256-byte step), lists spanning many steps, an 11-byte varint mid-list
+    (per-lane redo), empty lists and float lists between the int64 bodies: bit-exact vs the oracle."""
+    from tests.golden.gen_golden import enc, entry, example, f32, i64, ld
+
+    rng = np.random.default_rng(23)
+    pl = []
+    for i in range(400):
+        ents = []
+        for j in range(int(rng.integers(2, 9))):
+            m = int(rng.choice([0, 1, 5, 64, 200, 400]))
+            if j % 3 == 0:
+                v = [int(x) for x in rng.integers(0, 128, m)]  # 1-byte varints
+            else:
+                v = [int(x) for x in rng.integers(-(2**40), 2**40, m)]
+            feat = i64(*v)
+            if i % 17 == 4 and j == 1 and m > 3:  # an 11-byte varint in the middle of the body
+                raw = b"".join(enc(x) for x in v[:2]) + b"\xff" * 10 + b"\x01" + b"".join(enc(x) for x in v[2:])
+                feat = ld(3, ld(1, raw))
+            ents.append(entry(f"k{j}".encode(), feat))
+            if rng.random() < 0.3:
+                ents.append(entry(f"f{j}".encode(), f32(*rng.standard_normal(int(rng.integers(0, 20))).astype(np.float32).tolist())))
+        if i % 2:
+            rng.shuffle(ents)
+        pl.append(example(*ents))
+    buf, st, en = synth.framed(pl)
+    d = hip.HipDecoder(0)
+    try:
+        d.set_lane_max(0)
+        r = d.decode(buf, st, en)
+        assert r.info.n_big == len(pl)
+        bad = _compare_to_oracle(r, orc, buf, st, en)
+    finally:
+        d.close()
+    assert not bad, bad[:10]
+
+
 def test_long_int64_lists_spec_mode():
     """Same records with spec (64-bit) varints: the long lists decode to the encoded values."""
     pl, vals = _long_int_payloads(120, seed=19)
