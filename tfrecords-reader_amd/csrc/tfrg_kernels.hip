@@ -3069,9 +3069,11 @@ __device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bo
     rb += avail;
     if (rb >= kRingN) rb -= kRingN;
   };
+  uint32_t wn = Q0 + 4u * lane < Qend ? L32[(Q0 >> 2) + lane] : 0u;  // (each step's dword read one step ahead)
   for (uint32_t Qw = Q0; Qw < Qend; Qw += 256u) {
     const uint32_t Q = Qw + 4u * lane;
-    const uint32_t w = Q < Qend ? L32[Q >> 2] : 0u;
+    const uint32_t w = wn;
+    wn = Q + 256u < Qend ? L32[(Q + 256u) >> 2] : 0u;
     uint32_t bm = 0, ks = 0;  // bytes of this dword inside an eligible body (bodies are >= 8 bytes apart)
     uint64_t mw = __ballot(iv && bs < Qw + 256u && be > Qw);  // bodies overlapping this step
     while (mw) {
