@@ -3122,7 +3122,7 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
-  constexpr int kFG = 4;
+  constexpr int kFG = 8;
   uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
   while (m) {
     uint32_t fb[kFG], fn[kFG];
