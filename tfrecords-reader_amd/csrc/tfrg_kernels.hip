@@ -2659,13 +2659,15 @@ __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema
 // single values kept inline by the count pass are written straight from the loc word, other lists of
 // records <= lane_max are decoded from the wave's LDS stage. Records above lane_max belong to the
 // wavefront gather kernels, which run next and read these row splits.
-constexpr uint32_t kDG = 2;   // slots per scan group
 // kDT tiles per workgroup: kDT x kDG (count, loc) loads in flight per thread (4 for large batches,
 // 1 when that would leave CUs idle)
 
 template <bool COMPAT, uint32_t kDT>
 __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchema sc, DevOut o, uint32_t lane_max,
                                                             uint32_t n_tiles) {
+  // slots per scan group (one barrier each): 2 beside 4 tiles per workgroup, 8 with one tile (small
+  // batches and wide schemas: fewer barriers between the loads, same registers)
+  constexpr uint32_t kDG = kDT == 1 ? 8u : 2u;
   __shared__ uint32_t s_w[2][kDT * kDG][4];  // wave totals, double-buffered across slot groups
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t S = sc.n_slots;
