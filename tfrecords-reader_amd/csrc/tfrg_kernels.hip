@@ -1860,45 +1860,8 @@ __device__ __forceinline__ uint4 chunk_mask(uint4 w, uint64_t q, uint64_t a, uin
   return make_uint4(ws[0], ws[1], ws[2], ws[3]);
 }
 
-// chunk_u of an interior chunk (no masks) with the slice-by-16 tables at LDS address 0: all 16
-// table reads issued before the one wait (one LDS round trip per chunk; the compiler's schedule
-// drained them in two halves), in a single asm block so that no result is read before the wait.
-// Each read overwrites its own address register (16 VGPRs, not 32).
-__device__ __forceinline__ uint32_t chunk_u16_lds0(uint4 w) {
-  // byte extraction inside the block too: left to the scheduler, the 16 offsets of every chunk of a
-  // group were computed ahead of the first read (64 live VGPRs, spills)
-  uint32_t r[16];
-  const uint32_t two = 2u;
+// x << 2 with an SDWA byte select of x: a table byte offset in one VALU (the multiply-table lookups)
 #define TFRG_SDWA(o, two, src, k) "v_lshlrev_b32_sdwa %" #o ", %" #two ", %" #src " dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_" #k "\n\t"
-  asm volatile(
-      TFRG_SDWA(0, 16, 17, 0) TFRG_SDWA(1, 16, 17, 1) TFRG_SDWA(2, 16, 17, 2) TFRG_SDWA(3, 16, 17, 3)
-      TFRG_SDWA(4, 16, 18, 0) TFRG_SDWA(5, 16, 18, 1) TFRG_SDWA(6, 16, 18, 2) TFRG_SDWA(7, 16, 18, 3)
-      TFRG_SDWA(8, 16, 19, 0) TFRG_SDWA(9, 16, 19, 1) TFRG_SDWA(10, 16, 19, 2) TFRG_SDWA(11, 16, 19, 3)
-      TFRG_SDWA(12, 16, 20, 0) TFRG_SDWA(13, 16, 20, 1) TFRG_SDWA(14, 16, 20, 2) TFRG_SDWA(15, 16, 20, 3)
-      "ds_read_b32 %0, %0 offset:15360\n\t"
-      "ds_read_b32 %1, %1 offset:14336\n\t"
-      "ds_read_b32 %2, %2 offset:13312\n\t"
-      "ds_read_b32 %3, %3 offset:12288\n\t"
-      "ds_read_b32 %4, %4 offset:11264\n\t"
-      "ds_read_b32 %5, %5 offset:10240\n\t"
-      "ds_read_b32 %6, %6 offset:9216\n\t"
-      "ds_read_b32 %7, %7 offset:8192\n\t"
-      "ds_read_b32 %8, %8 offset:7168\n\t"
-      "ds_read_b32 %9, %9 offset:6144\n\t"
-      "ds_read_b32 %10, %10 offset:5120\n\t"
-      "ds_read_b32 %11, %11 offset:4096\n\t"
-      "ds_read_b32 %12, %12 offset:3072\n\t"
-      "ds_read_b32 %13, %13 offset:2048\n\t"
-      "ds_read_b32 %14, %14 offset:1024\n\t"
-      "ds_read_b32 %15, %15\n\t"
-      "s_waitcnt lgkmcnt(0)"
-      : "=&v"(r[0]), "=&v"(r[1]), "=&v"(r[2]), "=&v"(r[3]), "=&v"(r[4]), "=&v"(r[5]), "=&v"(r[6]), "=&v"(r[7]),
-        "=&v"(r[8]), "=&v"(r[9]), "=&v"(r[10]), "=&v"(r[11]), "=&v"(r[12]), "=&v"(r[13]), "=&v"(r[14]),
-        "=&v"(r[15])
-      : "v"(two), "v"(w.x), "v"(w.y), "v"(w.z), "v"(w.w));
-  return xor3(xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], r[8])),
-              xor3(r[9], r[10], r[11]), xor3(r[12], r[13], r[14])) ^ r[15];
-}
 
 // Bank-conflict-free slice-by-16 (the streaming CRC's LDS layout): the 16 tables are laid out in
 // rows of 64 dwords, row e = entry e, column c holding T[(c + 1) & 15][e] (c < 47). Lane l reads its
