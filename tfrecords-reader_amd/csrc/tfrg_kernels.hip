@@ -594,7 +594,7 @@ struct LdsTab {
   }
   __device__ __forceinline__ uint32_t step4(uint32_t x) const {
     if constexpr (R == 1)  // table byte offsets in one SDWA instruction each (the lane kernel is VALU-bound)
-      return at4(3, byte_x4<0>(x)) ^ at4(2, byte_x4<1>(x)) ^ at4(1, byte_x4<2>(x)) ^ at4(0, byte_x4<3>(x));
+      return xor3(at4(3, byte_x4<0>(x)), at4(2, byte_x4<1>(x)), at4(1, byte_x4<2>(x))) ^ at4(0, byte_x4<3>(x));
     return (*this)(3, x & 0xffu) ^ (*this)(2, (x >> 8) & 0xffu) ^ (*this)(1, (x >> 16) & 0xffu) ^ (*this)(0, x >> 24);
   }
   __device__ __forceinline__ uint32_t step1(uint32_t c_, uint32_t byte) const {
