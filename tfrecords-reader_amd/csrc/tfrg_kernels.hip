@@ -2950,16 +2950,20 @@ __device__ __forceinline__ bool int64_balanced(const FastSrc& fs, const DevOut& 
   return !__ballot(bad);
 }
 
-// One varint whose bytes are stage [s, s + nb), nb in 1..10 (the caller knows where it ends): the
-// reference's compat shifts as varint_bf (decoder.pyx:34-50).
+// One varint at stage offset s whose length the caller has checked (1..10 bytes, its first byte
+// < 0x80 is its last): byte masks from the terminator bits, the reference's compat shifts as
+// varint_bf (decoder.pyx:34-50).
 template <bool COMPAT>
-__device__ __forceinline__ int64_t varint_known(const uint8_t* l, uint32_t s, uint32_t nb) {
+__device__ __forceinline__ int64_t varint_term(const uint8_t* l, uint32_t s) {
   const uint32_t sh = s & 3u;
   const uint32_t* W = reinterpret_cast<const uint32_t*>(l) + (s >> 2);
   const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
   const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
   const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-  const uint32_t m0 = bytes_mask(nb), m1 = nb > 4u ? bytes_mask(nb - 4u) : 0u, m2 = nb > 8u ? bytes_mask(nb - 8u) : 0u;
+  const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
+  const uint32_t m0 = t0 ^ (t0 - 1u);
+  const uint32_t m1 = t0 ? 0u : t1 ^ (t1 - 1u);
+  const uint32_t m2 = (t0 | t1) ? 0u : (t2 ^ (t2 - 1u)) & 0xffffu;
   const uint32_t x = vgroups(w0, m0), x1 = vgroups(w1, m1), x2 = vgroups(w2, m2);
   if (COMPAT) {
     const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
@@ -3027,7 +3031,7 @@ __device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bo
     const uint32_t nb = pe + 1u - s;  // (wraps huge when pe < s)
     const bool ok = act && vi < scn && nb - 1u < 10u && (vi + 1u < scn || pe + 1u == sbe);
     bad |= act && !ok;
-    const int64_t v = varint_known<COMPAT>(fs.l, ok ? s : 0u, ok ? nb : 1u);
+    const int64_t v = varint_term<COMPAT>(fs.l, ok ? s : 0u);
     const uint64_t at = (uint64_t)pd + vi;
     if (ok && at < o.cap_i64) o.i64[at] = v;
     gb += avail;
