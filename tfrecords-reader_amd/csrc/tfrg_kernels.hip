@@ -2059,7 +2059,8 @@ __device__ __forceinline__ CrcEnt crc_ent(const CrcWin& w, uint32_t k) {
 
 // the rounds [Rf, Rl] of window entry k, Horner sum S per lane: placed, combined with the other
 // waves' slices of the record, and, once complete, checked against the stored CRC
-__device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, const CrcWin& w, uint32_t win0,
+__device__ __forceinline__ void crc_flush(const uint8_t* lbase, const DevBatch& B, const DevOut& o, const CrcWin& w,
+                                       uint32_t win0,
                                        uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
                                        uint32_t n_slots, uint32_t lane) {
   const uint64_t bas = rl64(w.base, k);
@@ -2093,8 +2094,19 @@ __device__ __forceinline__ void crc_flush(const DevBatch& B, const DevOut& o, co
   const uint64_t b = rl64(w.b, k);
   const uint32_t r = rfl32(o.crc_rec[win0 + k]), verdict = o.verdict[r];
   const uint32_t z = (uint32_t)(16ull * (((b - 1) >> 4) + 1ull) - b);  // zero bytes padding the last chunk
-  const uint32_t c = ~gf_mul(t, cst[kCstUnshift + z]);
-  if (crc_mask(c) == load_u32_unaligned(B.bytes, b)) {
+  // t is the state after the payload and z zero bytes: instead of un-shifting t by x^(-8z) (a 32-step
+  // multiply), the stored CRC's state is advanced by the same z zero bytes through the slicing
+  // tables of the rotated layout (wave-uniform lookups: broadcasts) and compared with t
+  const uint32_t um = load_u32_unaligned(B.bytes, b) - kCrcMaskDelta;
+  uint32_t v = ~((um << 15) | (um >> 17));  // ~crc_mask^-1(stored)
+  auto rt = [&](uint32_t col, uint32_t e) {
+    return *reinterpret_cast<const uint32_t*>(lbase + kRotTabOff + (e << 8) + 4u * col);
+  };
+  uint32_t zz = z;
+  for (; zz >= 4u; zz -= 4u)  // 4 zero bytes: slice-by-4 (tables 3, 2, 1, 0 in columns 2, 1, 0, 15)
+    v = xor3(rt(2u, v & 0xffu), rt(1u, (v >> 8) & 0xffu), rt(0u, (v >> 16) & 0xffu)) ^ rt(15u, v >> 24);
+  for (; zz; --zz) v = (v >> 8) ^ rt(15u, v & 0xffu);
+  if (v == t) {
     if (lane == 0) o.verdict[r] = (uint8_t)(verdict | TFRG_V_DATA_CRC);
   } else if (B.flags & kFlagStrictCrc) {
     strict_reject(o, B.n, n_slots, r, verdict, lane, 64);
@@ -2257,7 +2269,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
         S = (tab_at0 ? mul_a1_lds(S) : mul_tab(A1, S)) ^ rc[d];
       }
       if (stop == g.n) break;
-      if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
       cur = next;
       Rf = g.r0 + stop;
       S = 0;
@@ -2267,7 +2279,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   uint64_t R = R0;
   while (R < R1) {
     if (R >= lim) {  // next window (R is its first entry's first round)
-      if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
       cur = -1;
       win0 += 63u;
       w = crc_win_load(B, o, win0, nrec, TR, lane);
@@ -2289,7 +2301,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
       if (!ga.n) break;
     }
   }
-  if (cur >= 0) crc_flush(B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
+  if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
   PHASE_MARK(q9);
   PHASE_ADD(25, q0, q9);
 }
