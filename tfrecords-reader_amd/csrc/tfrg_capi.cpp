@@ -131,7 +131,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
   // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
   // 32 round shifts x^(8192 * 2^k)
-  std::vector<uint32_t> tab(8192 + 16384 + 2048), cst(128);
+  std::vector<uint32_t> tab(8192 + 16384 + 2048 + 24 * 1024), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -149,6 +149,11 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   memcpy(tab.data() + 24576, M, 4096);
   crc_make_mul_tables(gf_xpow8(4096), M);
   memcpy(tab.data() + 25600, M, 4096);
+  // multiply by x^(8192 * 2^k), k < 24: a slice of a record split over waves shifted to its place
+  for (int k = 0; k < 24; ++k) {
+    crc_make_mul_tables(gf_xpow8(1024ull << k), M);
+    memcpy(tab.data() + 26624 + k * 1024, M, 4096);
+  }
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts

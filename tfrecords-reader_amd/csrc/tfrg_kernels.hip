@@ -1802,6 +1802,7 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
 constexpr int kCrcDepth = TFRG_CRC_DEPTH;
 constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
 constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
+constexpr uint32_t kPowTabOff = 26624;   // crc_tab: [24][4][256] multiply by x^(8192 * 2^k) (split-slice shifts)
 constexpr uint32_t kNumCst = 128;
 
 // U(0, 16-byte chunk at q) of the payload [a, b): bytes outside zeroed, the first 4 payload bytes
@@ -2009,14 +2010,6 @@ __device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t k) {
   return (uint32_t)__builtin_amdgcn_readlane((int)x, (int)k);
 }
 
-// x^(8192 j): the factors x^(8192 * 2^k) of the set bits of j, multiplied across lanes 0..31
-__device__ __forceinline__ uint32_t xpow_rounds(uint32_t j, const uint32_t* cst, uint32_t lane) {
-  uint32_t f = (lane < 32u && ((j >> (lane & 31u)) & 1u)) ? cst[kCstRoundPow + (lane & 31u)] : 0x80000000u;
-#pragma unroll
-  for (int m = 1; m < 32; m <<= 1) f = gf_mul(f, (uint32_t)__shfl_xor((int)f, m, 64));
-  return rfl32(f);
-}
-
 // The streaming-CRC window: lane k < 63 describes list entry win0 + k, lane 63 holds the next
 // window's first flat round (the bound of this one). Three 64-bit values per lane; everything else
 // about an entry is derived in scalar registers (crc_ent) or loaded at its flush: the fewer VGPRs,
@@ -2059,8 +2052,8 @@ __device__ __forceinline__ CrcEnt crc_ent(const CrcWin& w, uint32_t k) {
 
 // the rounds [Rf, Rl] of window entry k, Horner sum S per lane: placed, combined with the other
 // waves' slices of the record, and, once complete, checked against the stored CRC
-__device__ __forceinline__ void crc_flush(const uint8_t* lbase, const DevBatch& B, const DevOut& o, const CrcWin& w,
-                                       uint32_t win0,
+__device__ __forceinline__ void crc_flush(const uint8_t* lbase, const uint32_t* __restrict__ ptab, const DevBatch& B,
+                                       const DevOut& o, const CrcWin& w, uint32_t win0,
                                        uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
                                        uint32_t n_slots, uint32_t lane) {
   const uint64_t bas = rl64(w.base, k);
@@ -2069,7 +2062,15 @@ __device__ __forceinline__ void crc_flush(const uint8_t* lbase, const DevBatch& 
   uint32_t t = gf_mul(S, cst[lane]);
 #pragma unroll
   for (int m = 32; m >= 1; m >>= 1) t ^= (uint32_t)__shfl_xor((int)t, m, 64);
-  if (jlo) t = gf_mul(t, xpow_rounds(jlo, cst, lane));
+  if (jlo) {  // x x^(8192 jlo): one table multiply per set bit of jlo (wave-uniform: scalar loads)
+    uint32_t u = rfl32(t);
+    for (uint32_t kb = 0, jj = jlo; jj; ++kb, jj >>= 1) {
+      if (!(jj & 1u)) continue;
+      const uint32_t* M = ptab + (size_t)kb * 1024u;
+      u = M[u & 0xffu] ^ M[256u + ((u >> 8) & 0xffu)] ^ M[512u + ((u >> 16) & 0xffu)] ^ M[768u + (u >> 24)];
+    }
+    t = u;
+  }
   if (jlo != 0u || jtop != J - 1u) {  // a slice of a record split over waves
     // (rounds done << 32 | XOR of the slices) updated in ONE 64-bit compare-and-swap: the wave that
     // completes the rounds sees every other slice in the value it replaced, with no fence (an
@@ -2269,7 +2270,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
         S = (tab_at0 ? mul_a1_lds(S) : mul_tab(A1, S)) ^ rc[d];
       }
       if (stop == g.n) break;
-      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
       cur = next;
       Rf = g.r0 + stop;
       S = 0;
@@ -2279,7 +2280,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   uint64_t R = R0;
   while (R < R1) {
     if (R >= lim) {  // next window (R is its first entry's first round)
-      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
       cur = -1;
       win0 += 63u;
       w = crc_win_load(B, o, win0, nrec, TR, lane);
@@ -2301,7 +2302,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
       if (!ga.n) break;
     }
   }
-  if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
+  if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
   PHASE_MARK(q9);
   PHASE_ADD(25, q0, q9);
 }
