@@ -2224,6 +2224,18 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     } else if (!edge) {
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) rc[d] = chunk_u(g.wd[d], 64, 0, ~0ull, T);
+    } else if (tab_at0 && g.kd[0] == g.kd[kCrcDepth - 1]) {  // edge rounds of one record: its entry once
+      const CrcEnt e = crc_ent(w, g.kd[0]);
+      const uint64_t a = rl64(w.a, g.kd[0]), b = rl64(w.b, g.kd[0]);
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) {
+        uint4 x = g.wd[d];
+        if (g.rd[d] <= e.bas + 1u || g.rd[d] == e.bas + e.J - 1u) {
+          const uint64_t ch = e.E + 64ull * g.rd[d] - lane;
+          x = (int64_t)ch >= (int64_t)e.c0 ? chunk_mask(x, ch << 4, a, b) : make_uint4(0, 0, 0, 0);
+        }
+        rc[d] = chunk_rot(x, RR, lane);
+      }
     } else if (tab_at0) {  // edge rounds: masked chunks, the same conflict-free lookups
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) {
