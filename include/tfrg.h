@@ -193,7 +193,8 @@ int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);
  * next batch stages while this one decodes. tfrg_stream_wait blocks until the slot's batch is
  * enqueued and gives its record count (and records per piece); results are then read from
  * tfrg_stream_ctx(slot) with tfrg_result_info / _fetch / _device and stay valid until the next
- * submit to that slot. The pieces' memory must stay valid until tfrg_stream_wait returns. Set the
+ * submit to that slot. A slot is submitted again only after tfrg_stream_wait claimed its last batch
+ * (else TFRG_E_ARG). The pieces' memory must stay valid until tfrg_stream_wait returns. Set the
  * key table on both contexts (tfrg_set_schema) while their slots are idle.
  * ------------------------------------------------------------------------------------------- */
 typedef struct tfrg_stream tfrg_stream;
@@ -219,9 +220,13 @@ const uint8_t* tfrg_stream_host_buffer(tfrg_stream* s, int slot);
 int tfrg_stream_host_ranges(tfrg_stream* s, int slot, const uint64_t** starts, const uint64_t** ends);
 
 /* Measurement helper (achievable HBM read bandwidth next to the 8 TB/s spec): one
- * streaming read of d_bytes[0, nbytes) (16 B loads, nbytes a multiple of 16) on `stream`, XOR-folded
- * into the u32 at d_sink so the loads are live. Not part of the decode path. */
-int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream);
+ * streaming read of d_bytes[0, nbytes) (16 B nontemporal loads, nbytes a multiple of 16) on
+ * `stream`, XOR-folded into the u32 at d_sink so the loads are live. variant 0..3 picks the loads in
+ * flight per lane and the grid (4/16 blocks per CU, 8/8, 8/16, 16/4). Not part of the decode path. */
+int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream, int variant);
+
+/* Devices visible to libtfrg (hipGetDeviceCount); the multi-device host paths spread files over them. */
+int tfrg_device_count(void);
 
 #ifdef __cplusplus
 }

@@ -65,3 +65,63 @@ def test_lpt_shards_balanced_by_bytes(directory):
         loads = [shard.read_shard(shard.shard_paths(directory, r, world)).nbytes for r in range(world)]
         assert sum(loads) == sizes.sum()
         assert max(loads) - min(loads) <= sizes.max()
+
+
+def _shard_rows(sb: shard.ShardBatch, res: shard.ShardResult):
+    out = []
+    rows = sb.index_rows()
+    for r0, r1, r in res.parts:
+        for j in range(r1 - r0):
+            name, s, e = rows[r0 + j]
+            ent = raw_entries(r, j) if r.status[j] == 0 else None
+            out.append((name, s, e, int(r.status[j]), int(r.verdict[j]), repr(G.canon_entries(ent) if ent else ent)))
+    return out
+
+
+@pytest.mark.parametrize("batch_bytes", [1 << 18, 1 << 20])
+def test_shard_split_over_batches_device_and_host(directory, batch_bytes):
+    """One rank's shard decoded as several batches (one context each, two streams) from HBM and from
+    host memory: the same rows as the single-batch decode of the whole shard, hence the oracle
+    (test above)."""
+    import torch
+
+    sb = shard.read_shard(directory)
+    dec = hip.HipDecoder(0)
+    try:
+        whole = _rows(sb, dec.decode(sb.buf, sb.starts, sb.ends))
+    finally:
+        dec.close()
+    sd = shard.ShardDecoder(0, batch_bytes=batch_bytes, n_streams=2)
+    try:
+        plan = sd.plan(sb.starts, sb.ends, sb.nbytes)
+        assert len(plan) >= 3
+        assert (plan[1:, 0] == plan[:-1, 1]).all() and plan[0, 0] == 0 and plan[-1, 1] == len(sb)
+        host = _shard_rows(sb, sd.decode(sb.buf, sb.starts, sb.ends))
+        assert host == whole
+        rst, ren = sd.rebase(plan, sb.starts, sb.ends)
+        dev = torch.device("cuda", 0)
+        d_bytes = torch.zeros(((sb.nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
+        d_bytes[: sb.nbytes].copy_(torch.from_numpy(sb.buf))
+        d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
+        d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        sd2 = shard.ShardDecoder(0, batch_bytes=batch_bytes, n_streams=2)
+        try:
+            sd2.learn(plan, sb.buf, sb.starts, sb.ends)
+            streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+            for _ in range(2):  # twice: the second decode reuses every context's arena
+                sd2.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(),
+                                  streams=[s.cuda_stream for s in streams])
+            infos = sd2.infos(plan)
+            if any(i.n_miss_records for i in infos):  # keys past the learning sample (the flowers files)
+                sd2.decode(sb.buf, sb.starts, sb.ends)
+                sd2.learn(plan, sb.buf, sb.starts, sb.ends)
+                sd2.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(),
+                                  streams=[s.cuda_stream for s in streams])
+                infos = sd2.infos(plan)
+            assert not any(i.n_miss_records for i in infos)
+            dev_rows = _shard_rows(sb, sd2.fetch(plan, sb.buf, sb.starts, sb.ends))
+            assert dev_rows == whole
+        finally:
+            sd2.close()
+    finally:
+        sd.close()

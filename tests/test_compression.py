@@ -50,6 +50,24 @@ def test_plain_file_with_zlib_like_header_stays_plain(tmp_path):
     assert indexer.create_tfrecord_pointers_index(str(p)).tolist() == [[0, 0x9C78 + 16, 0x9C78]]
 
 
+@pytest.mark.parametrize("crc", [True, False])
+def test_plain_file_with_zlib_like_header_and_ragged_tail_stays_plain(tmp_path, crc):
+    """A first record of length 0x9c78 (file starts 78 9c) followed by more records and a few
+    trailing bytes: the length chain no longer tiles the file. With spec CRCs the first frame's
+    length CRC decides; with zero CRCs the failed inflate falls back to the plain image. Either
+    way every complete record is indexed as the reference's walk does."""
+    payloads = [b"\x0a" + b"x" * (0x9C78 - 1)] + synth.c1_payloads(3)
+    p = tmp_path / "zr.tfrecord"
+    writer.write_tfrecord(p, payloads, crc=crc)
+    raw = p.read_bytes() + b"\x01\x02\x03"
+    p.write_bytes(raw)
+    assert raw[:2] == b"\x78\x9c"
+    assert _io.file_image(str(p)).tobytes() == raw
+    assert not _io.is_compressed(str(p)) or not crc
+    ptrs = indexer.create_tfrecord_pointers_index(str(p))
+    assert ptrs.shape[0] == 4 and int(ptrs[0, 2]) == 0x9C78
+
+
 def test_concatenated_gzip_members(plain, tmp_path):
     p, pl = plain
     raw = p.read_bytes()

@@ -226,8 +226,8 @@ def test_load_ranges_bounds_slots_times_records(orc, tmp_path, monkeypatch):
     calls = []
     real = reader._decode_bounded
 
-    def spy(dec, buf, st, en):
-        for at, res in real(dec, buf, st, en):
+    def spy(dec, buf, st, en, **kw):
+        for at, res in real(dec, buf, st, en, **kw):
             calls.append((at, int(res.status.size)))
             yield at, res
 

@@ -92,3 +92,24 @@ def test_two_rank_gloo_sharded_directory(tmp_path):
     idx = indexer.create_index_for_directory(str(tmp_path))
     want = sorted(zip(idx["tfrecord_filename"], idx["tfrecord_start"], idx["tfrecord_end"]))
     assert [(r[0], r[1], r[2]) for r in whole] == want
+
+
+def test_plan_batches_properties():
+    from tfr_reader import shard
+
+    rng = np.random.default_rng(5)
+    lens = rng.integers(16, 5000, 20000).astype(np.uint64)
+    en = np.cumsum(lens, dtype=np.uint64) + np.uint64(7)
+    st = en - lens
+    for cap in (4096, 1 << 16, 1 << 20, 1 << 31):
+        plan = shard.plan_batches(st, en, cap, int(en[-1]))
+        assert plan[0, 0] == 0 and plan[-1, 1] == st.size and (plan[1:, 0] == plan[:-1, 1]).all()
+        assert (plan[:, 2] % 16 == 0).all()
+        for r0, r1, lo, hi in plan.tolist():
+            assert lo <= int(st[r0]) and hi >= int(en[r1 - 1])
+            assert hi - lo <= cap or r1 - r0 == 1
+        rs, re = shard.ShardDecoder.rebase(plan, st, en)
+        base = np.repeat(plan[:, 2], plan[:, 1] - plan[:, 0]).astype(np.uint64)
+        assert ((rs + base) == st).all() and ((re + base) == en).all()
+    with pytest.raises(ValueError):
+        shard.plan_batches(st[::-1].copy(), en[::-1].copy(), 4096)

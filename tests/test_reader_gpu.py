@@ -224,3 +224,37 @@ def test_columnar_index_falls_back_on_missing_key(tmp_path):
     writer.write_tfrecord(tmp_path / "m.tfrecord", pl)
     with pytest.raises(KeyError, match="not found"):
         indexer.create_simple_index(tmp_path, "label", {}, {"name": "?"})
+
+
+@pytest.mark.parametrize("columnar", [True, False])
+def test_index_fn_decodes_in_chunks_below_the_cap(tmp_path, monkeypatch, columnar):
+    """create_index_for_tfrecord decodes a file in record chunks below reader.MAX_BATCH_BYTES (the
+    per-call cap stands in for the 4 GiB device limit): the rows equal those of one whole-file
+    decode, columnar and per-record alike."""
+    from tfr_reader import hip
+    from tfr_reader import reader as R
+    from tfr_reader import synth
+
+    p = tmp_path / "big.tfrecord"
+    extra = [] if columnar else synth.c3_payloads(20, seed=2, max_len=6)
+    writer.write_tfrecord(p, synth.c1_payloads(3000) + extra)
+    if columnar:
+        f = indexer.SimpleIndexColumns("label", {i: {"name": f"c{i}"} for i in range(0, 1000, 2)}, {"name": "?"},
+                                       [("id", "image_id")])
+    else:
+        def f(feat):
+            return {"keys": len(feat.fields_names), "first": feat[feat.fields_names[0]].value[:1]}
+    whole = dict(indexer.create_index_for_tfrecord(str(p), f))
+    assert len(whole["tfrecord_start"]) == 3000 + len(extra)
+    monkeypatch.setattr(R, "MAX_BATCH_BYTES", 4096)
+    calls = []
+    orig = hip.HipDecoder.decode
+
+    def spy(self, buf, st, en, **kw):
+        calls.append(len(buf))
+        return orig(self, buf, st, en, **kw)
+
+    monkeypatch.setattr(hip.HipDecoder, "decode", spy)
+    chunked = dict(indexer.create_index_for_tfrecord(str(p), f))
+    assert chunked == whole
+    assert len(calls) > 10 and max(calls) <= 4096 + 16

@@ -42,9 +42,12 @@ def _by_record(batches):
     return out
 
 
-@pytest.mark.parametrize("materialize", [True, False])
-def test_stream_equals_per_file_decode(files, materialize):
-    sd = stream.StreamDecoder(0, batch_bytes=1 << 18, copy_threads=3, materialize_bytes=materialize)
+@pytest.mark.parametrize("materialize,devices", [(True, None), (False, None), (True, [0, 0]), (False, [0, 0, 0])])
+def test_stream_equals_per_file_decode(files, materialize, devices):
+    """devices=[0, 0]: two lanes (two tfrg_streams, four contexts) on one GPU, the multi-device
+    path's batch distribution and in-order merge."""
+    sd = stream.StreamDecoder(0, batch_bytes=1 << 18, copy_threads=3, materialize_bytes=materialize,
+                              devices=devices)
     try:
         batches = list(sd.batches(files))
     finally:

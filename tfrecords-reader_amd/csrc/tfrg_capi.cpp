@@ -823,8 +823,14 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
 
 }  // extern "C"
 
-int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream) {
+int tfrg_stream_read(const void* d_bytes, uint64_t nbytes, uint32_t* d_sink, void* stream, int variant) {
   if (!d_bytes || !d_sink || (nbytes & 15u)) return TFRG_E_ARG;
-  return tfrg::launch_stream_read(d_bytes, nbytes, d_sink, static_cast<hipStream_t>(stream)) == hipSuccess
+  return tfrg::launch_stream_read(d_bytes, nbytes, d_sink, static_cast<hipStream_t>(stream), variant) == hipSuccess
              ? 0 : TFRG_E_HIP;
+}
+
+int tfrg_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
 }

@@ -229,8 +229,19 @@ int tfrg_compression_of(const uint8_t* img, uint64_t size) {
   else if (size >= 2 && (img[0] & 0x0f) == 8 && (img[0] >> 4) <= 7 && (((uint32_t)img[0] << 8) | img[1]) % 31 == 0)
     kind = TFRG_COMPRESSION_ZLIB;
   // a header that looks compressed may still be the start of a plain image (a first record of
-  // length 0x..9c78 begins 78 9c): a length chain that tiles the file exactly means uncompressed
-  if (kind != TFRG_COMPRESSION_NONE && framing_exact(img, size)) kind = TFRG_COMPRESSION_NONE;
+  // length 0x..9c78 begins 78 9c): a length chain that tiles the file exactly, or a first length
+  // field whose masked CRC-32C (bytes 8..12) matches, means uncompressed (a deflate stream passing
+  // that check by chance has odds of 2^-32)
+  if (kind != TFRG_COMPRESSION_NONE) {
+    if (size >= 12) {
+      uint64_t len;
+      uint32_t stored;
+      memcpy(&len, img, 8);
+      memcpy(&stored, img + 8, 4);
+      if (len <= size && stored == tfrg_masked_crc32c(img, 8)) return TFRG_COMPRESSION_NONE;
+    }
+    if (framing_exact(img, size)) kind = TFRG_COMPRESSION_NONE;
+  }
   return kind;
 }
 

@@ -193,7 +193,7 @@ enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageSpine, kStageDown
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.
-hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st);
+hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant);
 hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
                          const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream,
                          hipEvent_t* ev);

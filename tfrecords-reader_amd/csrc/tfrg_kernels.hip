@@ -3399,28 +3399,43 @@ hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o
   return launch_all<true>(b, sc, o, cfg, d_tab, d_consts, st, ev);
 }
 
-// Streaming read (measurement only): grid-stride 16 B loads, 4 in flight per lane.
-__global__ __launch_bounds__(256) void k_stream_read(const uint4* __restrict__ p, uint64_t n16, uint32_t* sink) {
+// Streaming read (measurement only): each block reads a contiguous slab, U 16-byte loads in flight
+// per lane (all issued before any is consumed), nontemporal (the data is not reused).
+typedef uint32_t sr_u32x4 __attribute__((ext_vector_type(4)));
+template <int U>
+__global__ __launch_bounds__(256) void k_stream_read(const sr_u32x4* __restrict__ p, uint64_t n16, uint32_t* sink) {
   uint32_t acc = 0;
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i + 3 * stride < n16; i += 4 * stride) {
-    const uint4 a = p[i], b = p[i + stride], c = p[i + 2 * stride], d = p[i + 3 * stride];
-    acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+  const uint64_t per_block = (n16 + gridDim.x - 1) / gridDim.x;
+  const uint64_t b0 = (uint64_t)blockIdx.x * per_block;
+  const uint64_t b1 = b0 + per_block < n16 ? b0 + per_block : n16;
+  uint64_t i = b0 + threadIdx.x;
+  for (; i + (U - 1) * 256 < b1; i += U * 256) {
+    sr_u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = __builtin_nontemporal_load(p + i + u * 256);
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
   }
-  for (; i < n16; i += stride) {
-    const uint4 a = p[i];
+  for (; i < b1; i += 256) {
+    const sr_u32x4 a = p[i];
     acc ^= a.x ^ a.y ^ a.z ^ a.w;
   }
   if (acc == 0x9e3779b9u) atomicXor(sink, acc);  // practically never taken; keeps the loads live
 }
 
-hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st) {
+// variant: 0 = 4 loads in flight, 16 blocks per CU; 1 = 8 loads, 8 blocks per CU; 2 = 8 loads, 16
+// blocks per CU; 3 = 16 loads, 4 blocks per CU (bench.py reports the fastest)
+hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant) {
   int dev = 0, cus = 256;
   (void)hipGetDevice(&dev);
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  hipLaunchKernelGGL(k_stream_read, dim3(cus * 8), dim3(256), 0, st, static_cast<const uint4*>(d), nbytes / 16,
-                     sink);
+  const sr_u32x4* q = static_cast<const sr_u32x4*>(d);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL(k_stream_read<4>, dim3(cus * 16), dim3(256), 0, st, q, nbytes / 16, sink); break;
+    case 1: hipLaunchKernelGGL(k_stream_read<8>, dim3(cus * 8), dim3(256), 0, st, q, nbytes / 16, sink); break;
+    case 2: hipLaunchKernelGGL(k_stream_read<8>, dim3(cus * 16), dim3(256), 0, st, q, nbytes / 16, sink); break;
+    default: hipLaunchKernelGGL(k_stream_read<16>, dim3(cus * 4), dim3(256), 0, st, q, nbytes / 16, sink); break;
+  }
   return hipGetLastError();
 }
 

@@ -233,7 +233,13 @@ static int stage_and_decode(tfrg_stream* s, const Job& j, double* ph) {
   }
   const int rc = tfrg_decode_device(s->ctx[k], s->d_buf[k], total, s->d_se[k], s->d_se[k] + s->max_rec, (uint32_t)n,
                                     j.flags, s->stream[k]);
-  if (!rc && hipStreamSynchronize(s->stream[k]) != hipSuccess) return TFRG_E_HIP;
+  if (!rc) {
+    const hipError_t e = hipStreamSynchronize(s->stream[k]);
+    if (e != hipSuccess) {
+      set_error(std::string("decode stream synchronize: ") + hipGetErrorString(e));
+      return TFRG_E_HIP;
+    }
+  }
   ph[2] = ms_since(t);
   return rc;
 }
@@ -394,8 +400,9 @@ int tfrg_stream_submit(tfrg_stream* s, int slot, const uint8_t* const* pieces, c
   }
   {
     std::unique_lock<std::mutex> lk(s->m);
-    if (s->state[slot] == kStaging) {
-      set_error("slot busy: wait for it first");
+    if (s->state[slot] != kFree) {  // staging, or a result / failure nobody has waited for yet
+      set_error(s->state[slot] == kStaging ? "slot busy: wait for it first"
+                                           : "slot holds an unclaimed result: tfrg_stream_wait it first");
       return TFRG_E_ARG;
     }
     s->state[slot] = kStaging;

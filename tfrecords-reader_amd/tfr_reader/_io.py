@@ -72,7 +72,18 @@ def file_image(path: str) -> np.ndarray:
     img = _mmap(path)
     if not _header_candidate(img[:2].tobytes()) or compression_of(img) == NONE:
         return img
-    out = inflate(img)
+    try:
+        out = inflate(img)
+    except N.NativeError:
+        # only the two header bytes said "compressed": if the first length field frames a record
+        # inside the file (a plain file with zero CRCs, a first length that reads as a zlib header
+        # and a ragged tail), read it as the plain file it then is, as the reference's fseek walk
+        # would (indexer.pyx:225-249); a truncated deflate stream (its "length" is its header and
+        # first deflate bytes, far past EOF) still raises
+        first = int(img[:8].view(np.uint64)[0]) if img.size >= 8 else 1 << 63
+        if first + 16 <= img.size:
+            return img
+        raise
     out.setflags(write=False)
     with _CACHE_LOCK:
         _CACHE[key] = out

@@ -80,7 +80,8 @@ SIGNATURES: dict[str, tuple] = {
                                        C.c_uint32]),
     "tfrg_template_count": (C.c_int, [C.c_void_p]),
     "tfrg_ctx_set_templates": (C.c_int, [C.c_void_p, C.c_int]),
-    "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]),
+    "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]),
+    "tfrg_device_count": (C.c_int, []),
     "tfrg_stream_create": (C.c_int, [C.c_int, C.c_uint64, C.c_int, C.POINTER(C.c_void_p)]),
     "tfrg_stream_destroy": (C.c_int, [C.c_void_p]),
     "tfrg_stream_ctx": (C.c_void_p, [C.c_void_p, C.c_int]),

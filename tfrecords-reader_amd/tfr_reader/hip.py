@@ -43,10 +43,15 @@ class KeyTable:
         self.slot_key: list[int] = []
         self.slot_kind: list[int] = []
         self.version = 0
+        self.lock = threading.RLock()  # (decoders of several host threads may share one table)
 
     def intern(self, key: bytes, kind: int) -> bool:
         """Add key (and its (key, kind) slot when kind != 0 and the key is valid UTF-8).
         Returns True if anything new was added."""
+        with self.lock:
+            return self._intern(key, kind)
+
+    def _intern(self, key: bytes, kind: int) -> bool:
         new = False
         kid = self.key_ids.get(key)
         if kid is None:
@@ -149,6 +154,10 @@ class HipDecoder:
         kt = self.keys
         if self._pushed == kt.version:
             return
+        with kt.lock:
+            self._push_schema(kt)
+
+    def _push_schema(self, kt: KeyTable) -> None:
         blob = b"".join(kt.keys)
         offs = np.zeros(len(kt.keys) + 1, np.uint64)
         if kt.keys:
@@ -244,7 +253,8 @@ class HipDecoder:
                     raise N.NativeError("row-split scan look-back timed out")
                 if info.n_miss_records == 0:
                     break
-                if not self._learn_misses(buf, info):
+                # (another decoder sharing the key table may have interned the keys first)
+                if not self._learn_misses(buf, info) and self._pushed == self.keys.version:
                     raise N.NativeError("schema misses reported but no new key learned")
             return self._fetch(buf, st, en, info, payload_only, materialize_bytes)
 

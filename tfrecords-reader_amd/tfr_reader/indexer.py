@@ -1,8 +1,9 @@
 """Dataset index builders (reference: src/tfr_reader/indexer.py).
 
 Offsets come from the native framing index (cython/indexer.py -> libtfrg), with the reference's
-``.idx`` caching side effect. When an ``index_fn`` is given, all records of a file are decoded in
-one device batch and ``index_fn`` runs on each decoded ``Feature`` in record order.
+``.idx`` caching side effect. When an ``index_fn`` is given, the records of a file are decoded in
+device batches below the per-call input cap and ``index_fn`` runs on each decoded ``Feature`` in
+record order (or once per batch on its columns, for a columnar ``index_fn``).
 """
 
 from __future__ import annotations
@@ -112,18 +113,24 @@ def create_index_for_tfrecord(tfrecord_path: str, index_fn: example.IndexFunc | 
     data["tfrecord_start"].extend(ptrs[:, 0].tolist())
     data["tfrecord_end"].extend(ptrs[:, 1].tolist())
     if index_fn is not None and n:
+        from tfr_reader.reader import _decode_bounded  # noqa: PLC0415 (reader imports this module)
+
         img = _io.file_image(tfrecord_path)
         ok = ptrs[:, 1] <= img.size
-        res = hip.default_decoder().decode(img, ptrs[:, 0], ptrs[:, 1]) if ok.any() else None
-        if getattr(index_fn, "columnar", False) and ok.all() and not res.status.any():
-            for key, value in index_fn(res).items():
-                data[key].extend(value)
-        else:
-            for i in range(n):
-                if not ok[i]:  # indexer.pyx:161-163
+        columnar = getattr(index_fn, "columnar", False)
+        # record chunks below the per-call input cap (reader.MAX_BATCH_BYTES): a file of any size
+        # indexes, as the reference's per-record decode does (indexer.pyx:134-179)
+        for at, res in _decode_bounded(hip.default_decoder(), img, ptrs[:, 0], ptrs[:, 1]):
+            m = len(res)
+            if columnar and ok[at : at + m].all() and not res.status.any():
+                for key, value in index_fn(res).items():
+                    data[key].extend(value)
+                continue
+            for j in range(m):
+                if not ok[at + j]:  # indexer.pyx:161-163
                     raise OSError("Failed to read record data")
-                f = res.feature(i)
-                row = index_fn.per_record(f) if getattr(index_fn, "columnar", False) else index_fn(f)
+                f = res.feature(j)
+                row = index_fn.per_record(f) if columnar else index_fn(f)
                 for key, value in row.items():
                     data[key].append(value)
     reader.close()

@@ -31,18 +31,29 @@ SLOT_BUDGET_BYTES = 4 << 30
 SLOT_COLUMN_BYTES = 18
 
 
-def _decode_bounded(dec, buf: np.ndarray, st: np.ndarray, en: np.ndarray):
+def _decode_bounded(dec, buf: np.ndarray, st: np.ndarray, en: np.ndarray, **kw):
     """dec.decode over record chunks of at most SLOT_BUDGET_BYTES / (18 x slots) records (the slot
-    count known before each chunk; a chunk that learns many new keys only shrinks the next ones).
+    count known before each chunk; a chunk that learns many new keys only shrinks the next ones)
+    and at most MAX_BATCH_BYTES of input each. Each chunk passes only its own byte span (16-byte
+    aligned base, offsets rebased), so the host->HBM copy per call is the chunk, not the buffer.
     Yields (first record index, BatchResult)."""
     n = st.size
     at = 0
+    top = np.maximum.accumulate(np.maximum(en, st)) if n else en
     while at < n:
         slots = max(1, len(dec.keys.slot_key))
         k = max(1024, SLOT_BUDGET_BYTES // (SLOT_COLUMN_BYTES * slots))
         if slots < 64:  # (a schema still being learned: a first chunk of bounded size)
             k = min(k, 1 << 16)
-        yield at, dec.decode(buf, st[at : at + k], en[at : at + k])
+        s, e = st[at : at + k], en[at : at + k]
+        lo = int(s.min()) & ~15
+        if (np.diff(s.astype(np.int64)) >= 0).all():  # (sorted ranges: cut where the span ends)
+            cut = int(np.searchsorted(top[at : at + k], np.uint64(lo + MAX_BATCH_BYTES), side="right"))
+            k = max(1, cut)
+            s, e = s[:k], e[:k]
+        hi = min(int(e.max()), buf.size)
+        base = np.uint64(lo)
+        yield at, dec.decode(buf[lo:max(hi, lo)], s - base, e - base, **kw)
         at += k
 
 
@@ -54,11 +65,11 @@ def _check_path(path) -> None:
         raise FileNotFoundError(f"Path {p} does not exist.")
 
 
-def _decode_framed_bytes(data: bytes, start: int, end: int) -> example.Feature:
+def _decode_framed_bytes(data: bytes, start: int, end: int, dec=None) -> example.Feature:
     """Decode the framed record held in ``data`` (the bytes read for [start, end))."""
     if example.feature.TFRECORD_READER_DECODER_IMP == "protobuf":
         return example.decode(data[12:-4])
-    r = hip.default_decoder().decode(data, [0], [end - start])
+    r = (dec or hip.default_decoder()).decode(data, [0], [end - start])
     return r.feature(0)
 
 
@@ -95,7 +106,32 @@ class TFRecordFileReader:
         return False
 
 
-def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]) -> list[example.Feature]:
+#: device list used when a caller passes devices=None (tfr_reader.set_devices)
+_DEFAULT_DEVICES = None
+_LANE_DECODERS: dict = {}
+
+
+def set_devices(devices) -> None:
+    """Default devices of ``load_ranges`` / ``load_records`` / ``__getitem__(Iterable)``: None (device
+    0), "all", an int or a list of device indices (tfr_reader.shard.resolve_devices)."""
+    global _DEFAULT_DEVICES
+    from tfr_reader import shard
+
+    _DEFAULT_DEVICES = None if devices is None else shard.resolve_devices(devices)
+
+
+def _lane_decoder(lane: int, device: int):
+    """The decode context of lane `lane` on `device` (lane 0: the module default of the device)."""
+    if lane == 0:
+        return hip.default_decoder(device)
+    d = _LANE_DECODERS.get((lane, device))
+    if d is None:
+        d = _LANE_DECODERS[(lane, device)] = hip.HipDecoder(device)
+    return d
+
+
+def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int],
+                devices=None) -> list[example.Feature]:
     """Decode framed records given as (file, start, end), in order, in device batches.
 
     Records are grouped by file. A file whose selected bytes are a large part of it is decoded
@@ -103,8 +139,13 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
     sparser selections are staged back to back by the native gather (tfrg_gather_ranges) into
     batches of up to MAX_BATCH_BYTES. Raises the exception of the first failing record in order,
     like the reference's ordered ``ThreadPoolExecutor.map`` (reader.py:246-247).
+
+    ``devices`` (default: ``set_devices``, else device 0): with several, the files are spread over
+    them by LPT on their selected bytes, one host thread and decode context per entry (the
+    reference's thread pool over records, reader.py:242-247, and process pool over files,
+    indexer.py:121-134); results are merged back into selection order.
     """
-    from tfr_reader import _native as N
+    from tfr_reader import shard
 
     n = len(paths)
     out: list = [None] * n
@@ -119,7 +160,31 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
     by_file: dict[str, list[int]] = {}
     for i, p in enumerate(paths):
         by_file.setdefault(p, []).append(i)
-    dec = hip.default_decoder()
+    items = [(p, np.asarray(ii, np.int64)) for p, ii in by_file.items()]
+    devs = shard.resolve_devices(devices if devices is not None else _DEFAULT_DEVICES)
+    if len(devs) == 1 or len(items) == 1:
+        _load_files(_lane_decoder(0, devs[0]), items, starts, ends, out, errors)
+    else:
+        from concurrent.futures import ThreadPoolExecutor
+
+        sel = [int((ends[ii] - starts[ii]).sum()) for _, ii in items]
+        parts = shard.lpt_partition(sel, len(devs))
+
+        def lane(k: int) -> None:
+            if parts[k]:
+                _load_files(_lane_decoder(k, devs[k]), [items[j] for j in parts[k]], starts, ends, out, errors)
+
+        with ThreadPoolExecutor(len(devs)) as ex:
+            list(ex.map(lane, range(len(devs))))
+    for i in range(n):
+        if errors[i] is not None:
+            raise errors[i]
+    return out
+
+
+def _load_files(dec, items, starts: np.ndarray, ends: np.ndarray, out: list, errors: list) -> None:
+    """load_ranges' work for the (path, selection indices) items of one decode context."""
+    from tfr_reader import _native as N
 
     def take(res, idx: np.ndarray) -> None:
         il = idx.tolist()
@@ -155,11 +220,10 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
             take(res, idx[at : at + res.status.size])
         pend_img, pend_idx, pend_bytes = [], [], 0
 
-    for path, idxs in by_file.items():
+    for path, ii in items:
         _check_path(path)
         img = _io.file_image(path)  # (mmap, or the decompressed stream of a ZLIB / GZIP file)
         fsize = int(img.size)
-        ii = np.asarray(idxs, np.int64)
         s, e = starts[ii], ends[ii]
         bad = (s >= fsize) | (e <= s)
         for i in ii[bad].tolist():
@@ -167,7 +231,8 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
         short = ~bad & (e > fsize)
         for i in ii[short].tolist():  # short read: decode alone so its buffer ends where the file does
             try:
-                out[i] = _decode_framed_bytes(img[int(starts[i]) : fsize].tobytes(), int(starts[i]), int(ends[i]))
+                out[i] = _decode_framed_bytes(img[int(starts[i]) : fsize].tobytes(), int(starts[i]), int(ends[i]),
+                                              dec)
             except Exception as exc:  # noqa: BLE001 — re-raised in selection order
                 errors[i] = exc
         ok = ii[~bad & ~short]
@@ -175,7 +240,9 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
             continue
         sel = int((ends[ok] - starts[ok]).sum())
         if sel * 4 >= fsize and fsize <= MAX_BATCH_BYTES:  # dense selection: the image itself
-            for at, res in _decode_bounded(dec, img, starts[ok], ends[ok]):
+            # bytes values gathered on the device (materialize_bytes): the Features own copies, as the
+            # reference's bytes objects do, instead of views into a mapping the file may change under
+            for at, res in _decode_bounded(dec, img, starts[ok], ends[ok], materialize_bytes=True):
                 take(res, ok[at : at + res.status.size])
             continue
         for lo in range(0, ok.size, 1 << 20):  # sparse selection: staged back to back
@@ -187,10 +254,6 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
             pend_idx.append(part)
             pend_bytes += nb
     flush()
-    for i in range(n):
-        if errors[i] is not None:
-            raise errors[i]
-    return out
 
 
 class TFRecordDatasetReader:
@@ -281,12 +344,13 @@ class TFRecordDatasetReader:
     def query(self, sql_query: str):
         return self.ctx.execute(sql_query)
 
-    def load_records(self, selection, max_workers: int | None = None) -> list[example.Feature]:
+    def load_records(self, selection, max_workers: int | None = None, devices=None) -> list[example.Feature]:
         """Decode the records of an index selection, in selection order (one device batch per
-        <= 1 GiB of record bytes; ``max_workers`` is accepted for API compatibility)."""
+        <= 1 GiB of record bytes; ``max_workers`` is accepted for API compatibility). ``devices``:
+        spread the selection's files over several GPUs (``load_ranges``)."""
         cols = F.columns(selection, ["tfrecord_filename", "tfrecord_start", "tfrecord_end"])
         paths = [join_path(self.dataset_dir, f) for f in cols["tfrecord_filename"]]
-        return load_ranges(paths, cols["tfrecord_start"], cols["tfrecord_end"])
+        return load_ranges(paths, cols["tfrecord_start"], cols["tfrecord_end"], devices)
 
     def _load_or_cache_index(self, index_path: str):
         if self.index_cache_dir is None:

@@ -16,6 +16,28 @@ from collections.abc import Sequence
 import numpy as np
 
 
+def resolve_devices(devices) -> list[int]:
+    """Device list of the multi-device host paths: None -> [0]; "all" -> every visible device; an
+    int -> [it]; a sequence -> as given (repeats are separate lanes on one device)."""
+    if devices is None:
+        return [0]
+    if isinstance(devices, str):
+        if devices != "all":
+            raise ValueError(f"devices must be 'all', an int or a list of ints, not {devices!r}")
+        from tfr_reader import _native as N
+
+        n = int(N.lib().tfrg_device_count())
+        if n < 1:
+            raise RuntimeError("no HIP device visible")
+        return list(range(n))
+    if isinstance(devices, (int, np.integer)):
+        return [int(devices)]
+    out = [int(d) for d in devices]
+    if not out:
+        raise ValueError("devices is empty")
+    return out
+
+
 def lpt_partition(sizes: Sequence[int], world: int) -> list[list[int]]:
     """Indices of `sizes` per rank; each rank's list is in ascending index order."""
     if world < 1:
@@ -75,6 +97,193 @@ class ShardBatch:
         """(tfrecord_filename, tfrecord_start, tfrecord_end) per record, as the dataset index holds."""
         return [(self.names[f], int(s), int(e)) for f, s, e in
                 zip(self.file_of.tolist(), self.file_starts.tolist(), self.file_ends.tolist())]
+
+
+#: one decode call covers < 4 GiB of input (u32 byte views); a shard is decoded as record-range
+#: batches of at most this many bytes, each into its own context's result columns
+DEFAULT_BATCH_BYTES = 1 << 30
+
+
+def plan_batches(starts: np.ndarray, ends: np.ndarray, batch_bytes: int = DEFAULT_BATCH_BYTES,
+                 nbytes: int | None = None) -> np.ndarray:
+    """Cut records (non-decreasing starts: one shard image in file order) into contiguous runs
+    whose byte span is at most ``batch_bytes``. Returns rows (r0, r1, lo, hi): records [r0, r1)
+    read bytes [lo, hi), lo aligned down to 16 so a batch's base keeps the 16-byte alignment of the
+    image. ``nbytes`` (the image size) clamps a last record that runs past EOF (indexer.pyx:225-249
+    indexes it; it decodes as truncated)."""
+    st = np.ascontiguousarray(starts, np.uint64)
+    en = np.ascontiguousarray(ends, np.uint64)
+    n = int(st.shape[0])
+    if batch_bytes < 32 or batch_bytes >= 1 << 32:
+        raise ValueError("batch_bytes must be in [32, 2^32)")
+    if n and (np.diff(st.astype(np.int64)) < 0).any():
+        raise ValueError("plan_batches needs non-decreasing starts (one image in file order)")
+    top = np.maximum.accumulate(np.maximum(en, st)) if n else en
+    if nbytes is not None:
+        top = np.minimum(top, np.uint64(nbytes))
+    rows = []
+    r0 = 0
+    while r0 < n:
+        lo = int(st[r0]) & ~15
+        r1 = int(np.searchsorted(top, np.uint64(lo + batch_bytes), side="right"))
+        if r1 <= r0:
+            r1 = r0 + 1  # one record wider than a batch: alone (the device rejects it if >= 4 GiB)
+        r1 = min(r1, r0 + (1 << 30))
+        rows.append((r0, r1, lo, max(int(top[r1 - 1]), lo)))
+        r0 = r1
+    return np.array(rows, np.int64).reshape(-1, 4)
+
+
+class ShardResult:
+    """Results of a shard decoded as several batches: ``parts[k] = (r0, r1, BatchResult)``, record
+    r of the shard being record r - r0 of its batch. Records stay in shard order, i.e. (file name,
+    start) order for a ``ShardBatch`` (reader.py:158)."""
+
+    def __init__(self, parts: list) -> None:
+        self.parts = parts
+        self._first = np.array([p[0] for p in parts] + [parts[-1][1] if parts else 0], np.int64)
+
+    def __len__(self) -> int:
+        return int(self._first[-1])
+
+    def locate(self, i: int):
+        """(BatchResult, index inside it) of shard record i."""
+        if i < 0 or i >= len(self):
+            raise IndexError(i)
+        k = int(np.searchsorted(self._first, i, side="right")) - 1
+        return self.parts[k][2], i - self.parts[k][0]
+
+    @property
+    def status(self) -> np.ndarray:
+        return np.concatenate([p[2].status for p in self.parts]) if self.parts else np.zeros(0, np.int32)
+
+    @property
+    def verdict(self) -> np.ndarray:
+        return np.concatenate([p[2].verdict for p in self.parts]) if self.parts else np.zeros(0, np.uint8)
+
+    def feature(self, i: int):
+        r, j = self.locate(i)
+        return r.feature(j)
+
+    def features(self) -> list:
+        """Every record as a ``Feature``; raises the first failing record's exception, in order."""
+        out: list = []
+        for _, _, r in self.parts:
+            out += r.features()
+        return out
+
+
+class ShardDecoder:
+    """Decodes one rank's shard on one device as record-range batches (``plan_batches``) of at most
+    ``batch_bytes`` each: one decode context per batch, so every batch's result columns stay valid
+    together, and the batches spread over ``n_streams`` streams so one batch's kernel tails overlap
+    the next batch's work. All contexts share one key table. This is the per-device unit of the
+    file-sharded directory decode: the reference reads a directory through a process
+    pool over files (indexer.py:121-134) and a thread pool over records (reader.py:212-247)."""
+
+    def __init__(self, device: int = 0, batch_bytes: int = DEFAULT_BATCH_BYTES, n_streams: int = 2,
+                 spec_varint: bool = False, keys=None) -> None:
+        from tfr_reader import hip
+
+        self.device = device
+        self.batch_bytes = int(batch_bytes)
+        self.n_streams = max(1, int(n_streams))
+        self.spec_varint = spec_varint
+        self.keys = keys or hip.KeyTable()
+        self.decs: list = []
+
+    def close(self) -> None:
+        for d in self.decs:
+            d.close()
+        self.decs = []
+
+    def _decoders(self, k: int) -> list:
+        from tfr_reader import hip
+
+        while len(self.decs) < k:
+            self.decs.append(hip.HipDecoder(self.device, self.spec_varint, keys=self.keys))
+        return self.decs[:k]
+
+    def plan(self, starts, ends, nbytes: int | None = None) -> np.ndarray:
+        return plan_batches(starts, ends, self.batch_bytes, nbytes)
+
+    # ------------------------------------------------------------------ host input
+    def decode(self, buf: np.ndarray, starts, ends, **kw) -> ShardResult:
+        """Decode records [starts[i], ends[i]) of one host image (non-decreasing starts), batch k on
+        context k; the streams' host threads run concurrently (ctypes releases the GIL). Keyword
+        arguments as ``HipDecoder.decode``."""
+        from concurrent.futures import ThreadPoolExecutor
+
+        buf = np.asarray(buf).reshape(-1).view(np.uint8)
+        st = np.ascontiguousarray(starts, np.uint64)
+        en = np.ascontiguousarray(ends, np.uint64)
+        plan = self.plan(st, en, buf.size)
+        decs = self._decoders(len(plan))
+        out: list = [None] * len(plan)
+
+        def one(k: int) -> None:
+            r0, r1, lo, hi = (int(x) for x in plan[k])
+            res = decs[k].decode(buf[lo:hi], st[r0:r1] - np.uint64(lo), en[r0:r1] - np.uint64(lo), **kw)
+            out[k] = (r0, r1, res)
+
+        if len(plan):  # the first batch learns the key set (and the record-shape templates) alone
+            one(0)
+
+        def run(t: int) -> None:
+            for k in range(1 + t, len(plan), self.n_streams):
+                one(k)
+
+        with ThreadPoolExecutor(self.n_streams) as ex:
+            list(ex.map(run, range(min(self.n_streams, max(1, len(plan))))))
+        return ShardResult(out)
+
+    # ------------------------------------------------------------------ device-resident input
+    @staticmethod
+    def rebase(plan: np.ndarray, starts, ends) -> tuple[np.ndarray, np.ndarray]:
+        """Per-batch offsets: record r of batch k as offsets from the batch base plan[k, 2]."""
+        st = np.ascontiguousarray(starts, np.uint64)
+        en = np.ascontiguousarray(ends, np.uint64)
+        base = np.repeat(plan[:, 2].astype(np.uint64), (plan[:, 1] - plan[:, 0]).astype(np.int64))
+        return st - base, en - base
+
+    def learn(self, plan: np.ndarray, buf: np.ndarray, starts, ends, sample: int = 4096) -> None:
+        """Key table and record-shape templates of every batch context from a host sample of the
+        first records (device-only callers; the host path learns them itself)."""
+        buf = np.asarray(buf).reshape(-1).view(np.uint8)
+        st = np.ascontiguousarray(starts, np.uint64)[:sample]
+        en = np.ascontiguousarray(ends, np.uint64)[:sample]
+        decs = self._decoders(len(plan))
+        if not decs or not st.size:
+            return
+        lo, hi = int(st[0]) & ~15, int(en.max())
+        decs[0].decode(buf[lo:hi], st - np.uint64(lo), en - np.uint64(lo))
+        for d in decs:
+            d.push_schema()
+            d.learn_templates(buf[lo:hi], st - np.uint64(lo), en - np.uint64(lo))
+
+    def decode_device(self, plan: np.ndarray, d_bytes: int, d_start: int, d_end: int, streams=None, **kw) -> None:
+        """Enqueue every batch of a device-resident shard: image at d_bytes (readable to its 16-byte
+        round-up), d_start / d_end the ``rebase``d offsets (u64 device arrays). Batch k runs on
+        ``streams[k % len(streams)]`` (HIP stream handles; default: each context's own stream)."""
+        decs = self._decoders(len(plan))
+        for k, (r0, r1, lo, hi) in enumerate(plan.tolist()):
+            s = streams[k % len(streams)] if streams else None
+            decs[k].decode_device(d_bytes + lo, hi - lo, d_start + 8 * r0, d_end + 8 * r0, r1 - r0, stream=s, **kw)
+
+    def infos(self, plan: np.ndarray) -> list:
+        """Decode summaries of the last ``decode_device`` (waits for it)."""
+        return [d.info() for d in self.decs[: len(plan)]]
+
+    def fetch(self, plan: np.ndarray, buf: np.ndarray, starts, ends) -> ShardResult:
+        """Host copies of the last ``decode_device``'s results (``buf``: the host image; bytes views
+        index it from each batch's base)."""
+        buf = np.asarray(buf).reshape(-1).view(np.uint8)
+        rs, re = self.rebase(plan, starts, ends)
+        parts = []
+        for k, (r0, r1, lo, _) in enumerate(plan.tolist()):
+            d = self.decs[k]
+            parts.append((r0, r1, d._fetch(buf[lo:], rs[r0:r1], re[r0:r1], d.info(), False)))
+        return ShardResult(parts)
 
 
 def read_shard(paths: Sequence[str]) -> ShardBatch:

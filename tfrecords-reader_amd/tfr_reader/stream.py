@@ -38,16 +38,29 @@ class StreamBatch:
 
 
 class StreamDecoder:
+    """``devices``: decode on several devices (a list of device indices, repeats allowed: two
+    entries of one device are two independent lanes on it; "all": every visible device). Batch k
+    goes to lane k % len(devices); batches are still yielded in plan order (file order, then record
+    order), so the output is the same whatever the lane count."""
+
     def __init__(self, device: int = 0, batch_bytes: int = 256 << 20, copy_threads: int = 8,
                  spec_varint: bool = False, materialize_bytes: bool = True, crc: bool = True,
-                 copy_results: bool = True) -> None:
+                 copy_results: bool = True, devices=None) -> None:
+        from tfr_reader import shard
+
         self._lib = N.lib()
-        h = C.c_void_p()
-        N.check(self._lib.tfrg_stream_create(device, batch_bytes, copy_threads, C.byref(h)), "tfrg_stream_create")
-        self._s = h
-        self.batch_bytes = batch_bytes
+        devs = shard.resolve_devices(devices) if devices is not None else [device]
         self.keys = hip.KeyTable()
-        self.dec = [hip.HipDecoder.wrap(self._lib.tfrg_stream_ctx(h, k), device, self.keys, spec_varint) for k in (0, 1)]
+        self._lanes = []  # (tfrg_stream handle, [decoder of slot 0, slot 1])
+        for d in devs:
+            h = C.c_void_p()
+            N.check(self._lib.tfrg_stream_create(d, batch_bytes, copy_threads, C.byref(h)), "tfrg_stream_create")
+            decs = [hip.HipDecoder.wrap(self._lib.tfrg_stream_ctx(h, k), d, self.keys, spec_varint) for k in (0, 1)]
+            self._lanes.append((h, decs))
+        self.devices = devs
+        self._s = self._lanes[0][0]
+        self.dec = self._lanes[0][1]
+        self.batch_bytes = batch_bytes
         self.materialize_bytes = materialize_bytes
         self.crc = crc
         self.copy_results = copy_results
@@ -55,9 +68,11 @@ class StreamDecoder:
 
     def close(self) -> None:
         """Frees the pinned buffers: results wrapped without ``copy_results`` are invalid after this."""
-        if self._s:
-            self._lib.tfrg_stream_destroy(self._s)
-            self._s = None
+        for h, _ in getattr(self, "_lanes", []):
+            if h:
+                self._lib.tfrg_stream_destroy(h)
+        self._lanes = []
+        self._s = None
 
     def __del__(self):  # noqa: D105
         try:
@@ -102,18 +117,19 @@ class StreamDecoder:
             yield cur
 
     # ------------------------------------------------------------------ run
-    def _submit(self, slot: int, pieces) -> None:
-        self.dec[slot].push_schema()
+    def _submit(self, lane: int, slot: int, pieces) -> None:
+        h, decs = self._lanes[lane]
+        decs[slot].push_schema()
         k = len(pieces)
         ptrs = (C.c_void_p * k)(*[pc[5].ctypes.data if pc[5] is not None else None for pc in pieces])
         names = (C.c_char_p * k)(*[pc[2].encode() if pc[2] is not None else None for pc in pieces])
         offs = np.array([pc[3] for pc in pieces], np.uint64)
         sizes = np.array([pc[4] for pc in pieces], np.uint64)
-        flags = self.dec[slot]._flags(False, self.crc, False, self.materialize_bytes)
-        N.check(self._lib.tfrg_stream_submit(self._s, slot, ptrs, names, N.ptr(offs, N.u64p), N.ptr(sizes, N.u64p), k,
+        flags = decs[slot]._flags(False, self.crc, False, self.materialize_bytes)
+        N.check(self._lib.tfrg_stream_submit(h, slot, ptrs, names, N.ptr(offs, N.u64p), N.ptr(sizes, N.u64p), k,
                                              flags), "tfrg_stream_submit")
 
-    def _finish(self, slot: int, pieces) -> StreamBatch:
+    def _finish(self, lane: int, slot: int, pieces) -> StreamBatch:
         import time
 
         t0 = time.perf_counter()
@@ -121,21 +137,22 @@ class StreamDecoder:
         nb = C.c_uint64()
         pr = np.zeros(len(pieces), np.uint64)  # (the pieces' images stay referenced until here)
         ms = (C.c_double * 4)()
-        N.check(self._lib.tfrg_stream_wait(self._s, slot, C.byref(n), C.byref(nb), N.ptr(pr, N.u64p), len(pieces),
+        h, decs = self._lanes[lane]
+        N.check(self._lib.tfrg_stream_wait(h, slot, C.byref(n), C.byref(nb), N.ptr(pr, N.u64p), len(pieces),
                                            ms), "tfrg_stream_wait")
-        d = self.dec[slot]
+        d = decs[slot]
         n_rec, nbytes = int(n.value), int(nb.value)
         d.push_schema()  # (keys learned from the other slot's batch)
-        hb = self._lib.tfrg_stream_host_buffer(self._s, slot)
+        hb = self._lib.tfrg_stream_host_buffer(h, slot)
         buf = np.ctypeslib.as_array(C.cast(hb, C.POINTER(C.c_uint8)), shape=(max(nbytes, 1),))[:nbytes]
         sp, ep = N.u64p(), N.u64p()
-        self._lib.tfrg_stream_host_ranges(self._s, slot, C.byref(sp), C.byref(ep))
+        self._lib.tfrg_stream_host_ranges(h, slot, C.byref(sp), C.byref(ep))
         st = np.ctypeslib.as_array(sp, shape=(max(n_rec, 1),))[:n_rec].copy()
         en = np.ctypeslib.as_array(ep, shape=(max(n_rec, 1),))[:n_rec].copy()
         t1 = time.perf_counter()
         info = N.TfrgInfo()
         cols = N.TfrgColumns()
-        N.check(self._lib.tfrg_stream_result(self._s, slot, C.byref(info), C.byref(cols)), "tfrg_stream_result")
+        N.check(self._lib.tfrg_stream_result(h, slot, C.byref(info), C.byref(cols)), "tfrg_stream_result")
         t2 = time.perf_counter()
         if info.n_miss_records:  # new keys (usually the first batch only): learn them, decode again
             res = d.decode(buf.copy(), st, en, crc=self.crc, materialize_bytes=self.materialize_bytes)
@@ -148,8 +165,10 @@ class StreamDecoder:
         return StreamBatch([(pc[0], pc[1]) for pc in pieces], pr.astype(int).tolist(), res, list(ms))
 
     def _wrap(self, d, cols, info, buf, st, en) -> hip.BatchResult:
-        """A BatchResult over the slot's pinned result columns (copied into numpy arrays only when
-        ``copy_results``; otherwise valid until the slot's next batch, i.e. two batches later)."""
+        """A BatchResult over the slot's pinned result columns, copied into numpy arrays when
+        ``copy_results`` (the default). Without it the arrays are views of the slot's pinned buffers,
+        valid only until the caller asks for the next batch: the slot is then handed its next batch
+        (and may reallocate its buffers)."""
         n, ns = info.n_records, info.n_slots
         kt = info.kind_totals
 
@@ -186,13 +205,15 @@ class StreamDecoder:
         return r
 
     def batches(self, paths: Iterable[str]) -> Iterator[StreamBatch]:
+        """Decoded batches in plan order. Up to two batches per lane are in flight (one staging
+        while the other decodes); batch k runs on lane k % lanes, slot (k // lanes) % 2."""
         pending: deque = deque()
-        slot = 0
-        for pieces in self._plan(paths):
-            if len(pending) == 2:
+        L = len(self._lanes)
+        for k, pieces in enumerate(self._plan(paths)):
+            if len(pending) == 2 * L:
                 yield self._finish(*pending.popleft())
-            self._submit(slot, pieces)
-            pending.append((slot, pieces))
-            slot ^= 1
+            lane, slot = k % L, (k // L) % 2
+            self._submit(lane, slot, pieces)
+            pending.append((lane, slot, pieces))
         while pending:
             yield self._finish(*pending.popleft())

@@ -26,8 +26,8 @@ def run_pass(out: Path, counter: str, config: str) -> Path:
            "-d", str(d), "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--only", config, "--no-cpu",
            "--steps", "3", "--warmup", "1", "--profile-steps", "1"]
     env = dict(os.environ, TMPDIR="/tmp")
-    with open(out / f"{counter}.log", "w") as log:
-        subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=env)
+    with open(out / f"{counter}.log", "w") as log, open(out / f"{counter}.err", "w") as err:
+        subprocess.run(cmd, check=True, stdout=log, stderr=err, env=env)
     return next(d.rglob("*counter_collection.csv"))
 
 
@@ -43,8 +43,11 @@ def main() -> None:
     out.mkdir(parents=True, exist_ok=True)
     name, fetch_kb = per_launch(run_pass(out, "FETCH_SIZE", config), want)
     _, write_kb = per_launch(run_pass(out, "WRITE_SIZE", config), want)
-    workload = {"c4": "c4_c1", "c4c2": "c4_c2"}.get(config, config)
-    res = {"config": workload, "kernel": name.split("(")[0], "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+    workload = {"c4": "c4_c1", "c4c2": "c4_c2", "c4of8": "c4_c1_rank0of8"}.get(config, config)
+    line = json.loads((out / "FETCH_SIZE.log").read_text().strip().splitlines()[-1])
+    records, launches = line["config"]["records_per_gpu"], line["config"]["batches_per_gpu"]
+    res = {"config": workload, "records": records, "launches_per_step": launches,
+           "kernel": name.split("(")[0], "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
            "traffic_bytes": fetch_kb * 1024 * 2 + write_kb * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 128-B fills tallied at 64 B), WRITE_SIZE as read"}
     (out / f"traffic_{workload}.json").write_text(json.dumps(res, indent=1))
