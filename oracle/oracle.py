@@ -63,9 +63,9 @@ class Oracle:
         except Exception:  # noqa: BLE001
             pass
 
-    def decode(self, payload: bytes, compat: bool = True):
+    def decode(self, payload: bytes, compat: bool = True, views: bool = False):
         """-> (status, aux, entries); entries = [(key bytes, kind name, values)] in dict order;
-        float values as raw u32 bits, bytes values as bytes."""
+        float values as raw u32 bits, bytes values as bytes (views: (offset in payload, length))."""
         L = lib()
         aux = C.c_int64()
         olen = C.c_int64()
@@ -95,7 +95,10 @@ class Oracle:
             else:
                 pairs = struct.unpack_from(f"<{2 * cnt}I", raw, p)
                 p += 8 * cnt
-                vals = [payload[pairs[2 * j] : pairs[2 * j] + pairs[2 * j + 1]] for j in range(cnt)]
+                if views:
+                    vals = [(pairs[2 * j], pairs[2 * j + 1]) for j in range(cnt)]
+                else:
+                    vals = [payload[pairs[2 * j] : pairs[2 * j] + pairs[2 * j + 1]] for j in range(cnt)]
             entries.append((key, KIND[kind], vals))
         return st, aux.value, entries
 

@@ -66,9 +66,8 @@ _ACCESSORS: dict[str, type[BaseFeature]] = {
 
 
 class Feature:
-    """All features of one example, keyed by name, in the record's key order."""
-
-    __slots__ = ("feature",)
+    """All features of one example, keyed by name, in the record's key order. (No ``__slots__``:
+    the device path's subclass is also a ``dict`` of accessors, tfr_reader/hip.py.)"""
 
     def __init__(self, feature):
         self.feature = feature

@@ -325,6 +325,7 @@ class BatchResult:
     bytes_data: np.ndarray | None = None  # materialize_bytes: the device-gathered byte column
     bytes_offsets: np.ndarray | None = None  # its u64 offsets (one per bytes element, + 1)
     _lay = None  # (record -> layout index, layouts), built on first use
+    _py = None  # per slot: (values as Python objects, rebased row splits), built on first use
 
     def _bytes_elems(self, lo: int, hi: int) -> list[bytes]:
         """bytes elements [lo, hi) of the bytes value array, as ``bytes``."""
@@ -379,20 +380,63 @@ class BatchResult:
 
     def feature(self, i: int):
         """Record i as a ``Feature`` (raises the record's exception)."""
-        from tfr_reader.example.feature import Feature  # noqa: PLC0415
-
         self.raise_for(i)
         if self._lay is None:
             self._lay = self._layouts()
         inv, layouts = self._lay
-        return Feature(_RecordView(self, i, layouts[int(inv[i])]))
+        if self._py is None:
+            self._py = [None] * len(self.slot_kind)
+        return _record_class()((self, i, layouts[int(inv[i])]))
+
+    def _pycol(self, s: int):
+        """Slot s over the whole batch as Python objects, converted once and cached: (the values of
+        the slot's column as a list, its row splits rebased to that list). A record's ``.value`` is
+        then one list slice (the fresh list the reference returns per access)."""
+        py = self._py
+        if py is None:
+            py = self._py = [None] * len(self.slot_kind)
+        c = py[s]
+        if c is None:
+            base = int(self.slot_base[s])
+            rs = self.row_splits[s]
+            r0 = int(rs[0])
+            lo, hi = base + r0, base + int(rs[-1])
+            kind = self.slot_kind[s]
+            if kind == 3:
+                vals = self.i64[lo:hi].tolist()
+            elif kind == 2:
+                vals = self.f32[lo:hi].view(np.float32).tolist()
+            else:
+                vals = self._bytes_list(lo, hi)
+            c = py[s] = (vals, (rs - np.uint32(r0)).tolist() if r0 else rs.tolist())
+        return c
+
+    def _bytes_list(self, lo: int, hi: int) -> list[bytes]:
+        """bytes elements [lo, hi) as ``bytes``, sliced from one bytes copy of the region they span."""
+        if hi <= lo:
+            return []
+        if self.bytes_data is not None:
+            o = self.bytes_offsets[lo : hi + 1]
+            a = int(o[0])
+            blob = self.bytes_data[a : int(o[-1])].tobytes()
+            ol = (o - np.uint64(a)).tolist()
+            return [blob[ol[j] : ol[j + 1]] for j in range(hi - lo)]
+        off = self.bytes_off[lo:hi]
+        ln = self.bytes_len[lo:hi]
+        a = int(off.min())
+        b = int((off.astype(np.uint64) + ln).max())
+        if b - a > 4 * (int(ln.sum()) + 64 * (hi - lo)):  # (scattered views: per-element copies)
+            return self._bytes_elems(lo, hi)
+        blob = self.buf[a:b].tobytes()
+        ol = (off - np.uint32(a)).tolist()
+        return [blob[x : x + n] for x, n in zip(ol, ln.tolist())]
 
     def _layouts(self) -> tuple[np.ndarray, list[_Layout]]:
         """Per record, the index of its key layout (present slots in dict order); records of a
         dataset share a handful of layouts, so the per-record work is one array lookup."""
         ns, n = self.order.shape
         if ns == 0:
-            return np.zeros(n, np.int64), [_Layout((), self.slot_key)]
+            return np.zeros(n, np.int64), [_Layout((), self.slot_key, self.slot_kind)]
         if ns <= 4:
             sig = np.zeros(n, np.uint64)
             for s in range(ns):
@@ -405,14 +449,13 @@ class BatchResult:
         layouts = []
         for col in cols:
             present = sorted((rk, s) for s, rk in enumerate(col) if rk)
-            layouts.append(_Layout(tuple(s for _, s in present), self.slot_key))
+            layouts.append(_Layout(tuple(s for _, s in present), self.slot_key, self.slot_kind))
         return inv.reshape(-1), layouts
 
     def features(self, start: int = 0, stop: int | None = None) -> list:
-        """Records [start, stop) as ``Feature`` objects (lazy column views). Raises the first
-        failing record's exception, in record order, like decoding them one by one."""
-        from tfr_reader.example.feature import Feature  # noqa: PLC0415
-
+        """Records [start, stop) as ``Feature`` objects (views over the batch's columns: a slot's
+        values become Python objects once per batch, on first access). Raises the first failing
+        record's exception, in record order, like decoding them one by one."""
         stop = len(self) if stop is None else min(stop, len(self))
         bad = np.flatnonzero(self.status[start:stop])
         if bad.size:
@@ -420,8 +463,11 @@ class BatchResult:
         if self._lay is None:
             self._lay = self._layouts()
         inv, layouts = self._lay
-        return [Feature(_RecordView(self, i, layouts[j]))
-                for i, j in zip(range(start, stop), inv[start:stop].tolist())]
+        if self._py is None:
+            self._py = [None] * len(self.slot_kind)
+        rec = _record_class()
+        # one (batch, record, layout) tuple per record (built by tuple.__new__: no Python __init__)
+        return [rec((self, i, layouts[j])) for i, j in zip(range(start, stop), inv[start:stop].tolist())]
 
     def column(self, key: str, kind: str | None = None) -> tuple[np.ndarray, np.ndarray]:
         """Ragged column of one key over the batch: (values, offsets) with record i's values at
@@ -453,12 +499,14 @@ class BatchResult:
 class _Layout:
     """Present slots of a record in dict order, with the key -> slot map they imply."""
 
-    __slots__ = ("slots", "keys", "index")
+    __slots__ = ("slots", "keys", "index", "acc")
 
-    def __init__(self, slots: tuple[int, ...], slot_key: list[str]) -> None:
+    def __init__(self, slots: tuple[int, ...], slot_key: list[str], slot_kind: list[int] | None = None) -> None:
         self.slots = slots
         self.keys = [slot_key[s] for s in slots]
         self.index = dict(zip(self.keys, slots))
+        # key -> (slot, accessor class) for the Feature fast path (_HipRecord.__getitem__)
+        self.acc = {k: (s, _accessor_classes()[slot_kind[s]]) for k, s in self.index.items()} if slot_kind else {}
 
 
 class _RecordView:
@@ -545,6 +593,135 @@ class ColumnFeature:
     @property
     def bytes_list(self) -> _ValueList:
         return self._list("bytes_list", "a")
+
+
+# ---------------------------------------------------------------------- Feature fast path
+_RECORD_CLASS = None
+_ACC_CLASSES = None
+
+
+class _ListRaw:
+    """A raw feature over one decoded list (``Feature.feature[key]`` of the fast path)."""
+
+    __slots__ = ("kind", "_v")
+
+    def __init__(self, kind: str, v: list) -> None:
+        self.kind, self._v = kind, v
+
+    def WhichOneof(self, _kind: str) -> str:  # noqa: N802 (protobuf API name)
+        return self.kind
+
+    def _list(self, want: str, article: str):
+        if self.kind != want:
+            raise Exception(f"Feature is not {article} {want}")  # noqa: TRY002
+        return _Values(self._v)
+
+    @property
+    def float_list(self):
+        return self._list("float_list", "a")
+
+    @property
+    def int64_list(self):
+        return self._list("int64_list", "an")
+
+    @property
+    def bytes_list(self):
+        return self._list("bytes_list", "a")
+
+
+class _Values:
+    __slots__ = ("_v",)
+
+    def __init__(self, v: list) -> None:
+        self._v = v
+
+    @property
+    def value(self) -> list:
+        return list(self._v)
+
+    def __getitem__(self, item):
+        return self._v[item]
+
+
+def _accessor_classes() -> dict:
+    """kind -> accessor class: ``Int64List`` / ``FloatList`` / ``BytesList`` subclasses over a slice
+    of a slot's cached Python list (``.value`` returns a fresh list, as the reference's does)."""
+    global _ACC_CLASSES
+    if _ACC_CLASSES is None:
+        from tfr_reader.example import feature as F  # noqa: PLC0415
+
+        def make(base, kind):
+            # a (values, lo, hi) tuple: created by tuple.__new__ alone (no Python __init__ per access)
+            class Acc(tuple, base):
+                __slots__ = ()
+                __init__ = tuple.__init__
+
+                @property
+                def value(self):
+                    return self[0][self[1] : self[2]]
+
+                @property
+                def feature(self):
+                    return _ListRaw(kind, self[0][self[1] : self[2]])
+
+            Acc.__name__ = Acc.__qualname__ = base.__name__
+            return Acc
+
+        _ACC_CLASSES = {3: make(F.Int64List, "int64_list"), 2: make(F.FloatList, "float_list"),
+                        1: make(F.BytesList, "bytes_list")}
+    return _ACC_CLASSES
+
+
+def _record_class():
+    """The device path's ``Feature``: a (BatchResult, record, layout) tuple (one C-level allocation
+    per record). ``f[key]`` builds the accessor (``Int64List`` / ``FloatList`` / ``BytesList`` over
+    a slice of the batch's cached per-slot Python list) and ``.value`` is one list slice; a missing
+    key raises the reference's KeyError (feature.py:88-92). ``.feature`` is the reference's
+    key -> raw feature mapping."""
+    global _RECORD_CLASS
+    if _RECORD_CLASS is None:
+        from tfr_reader.example.feature import Feature  # noqa: PLC0415
+
+        fields = tuple.__iter__  # (C-level unpacking: __getitem__ is the feature lookup here)
+
+        class HipFeature(tuple, Feature):
+            __slots__ = ()
+            __init__ = tuple.__init__
+            __eq__ = Feature.__eq__
+            __ne__ = lambda self, other: not self == other  # noqa: E731
+            __hash__ = None
+            __repr__ = Feature.__repr__
+
+            @property
+            def feature(self):  # the reference's key -> raw feature mapping
+                r, i, lay = fields(self)
+                return _RecordView(r, i, lay)
+
+            def __len__(self) -> int:
+                return len(tuple.__getitem__(self, 2).slots)
+
+            def __iter__(self):  # (the reference's Feature has no iteration of its own)
+                raise TypeError("'Feature' object is not iterable")
+
+            @property
+            def fields_names(self) -> list[str]:
+                return list(tuple.__getitem__(self, 2).keys)
+
+            def __getitem__(self, key: str):
+                r, i, lay = fields(self)
+                ent = lay.acc.get(key)
+                if ent is None:
+                    raise KeyError(f"Feature '{key}' not found in the example, expected one of {lay.keys}")
+                s, cls = ent
+                c = r._py[s]
+                if c is None:
+                    c = r._pycol(s)
+                rs = c[1]
+                return cls((c[0], rs[i], rs[i + 1]))
+
+        HipFeature.__name__ = HipFeature.__qualname__ = "Feature"
+        _RECORD_CLASS = HipFeature
+    return _RECORD_CLASS
 
 
 # ---------------------------------------------------------------------- module-level default engine
