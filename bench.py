@@ -230,6 +230,9 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> 
     present = _present_lists(sd.decs[0], w)
     side = [torch.cuda.Stream(dev) for _ in range(max(1, ctx.args.streams))]
     handles = [s.cuda_stream for s in side]
+    max_record = int((w.ends - w.starts).max())  # (the host knows its ranges: no large-record launch for C1)
+    for d in sd._decoders(len(plan)):
+        d.set_record_bound(max_record)
 
     def step(streams=handles):
         sd.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(), streams=streams)
@@ -315,6 +318,9 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> 
         # streaming payload CRC of the records above lane_max (their bytes + list entry and offsets);
         # the exact walker's slow list is empty on these workloads
         "k_tail_count": big_bytes + 32 * n_big,
+        # staged large records (<= 12 KiB): their framed bytes + offsets in; status, verdict and the
+        # order / count / loc words of every slot out
+        "k_stage_count": big_bytes + n_big * (16 + 5 + 14 * n_slots),
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         # out-of-line lists: every value written once (their record bytes are counted by the lanes)

@@ -97,6 +97,16 @@ int tfrg_ctx_create(int device, tfrg_ctx** out);
 int tfrg_ctx_destroy(tfrg_ctx* ctx);
 /* records larger than lane_max bytes take the wavefront-per-record kernels (default 2048) */
 int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
+/* Records above lane_max whose span fits the 12 KiB stage counted one wavefront per record from LDS
+ * (k_stage_count: entry-parallel canonical walk + lane-parallel payload CRC) instead of one lane
+ * per record from HBM plus the streaming CRC. Off by default (env TFRG_STAGE_COUNT=1): identical
+ * results, measured slower on the wide-schema config so far. */
+int tfrg_ctx_set_stage_count(tfrg_ctx* ctx, int on);
+/* An upper bound on (end - start) of the records of the following tfrg_decode_device calls (0 =
+ * unknown, the default). With a bound <= lane_max the batch has no large records and their count
+ * kernel is not launched (a few microseconds per decode); a wrong bound still decodes correctly
+ * (such records take the lane kernel's slower path). tfrg_decode_host derives it per call. */
+int tfrg_ctx_set_record_bound(tfrg_ctx* ctx, uint64_t max_record_bytes);
 /* wavefront records spanning <= nbytes are staged in LDS (clamped to the kernel's 12 KiB stage;
  * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
 int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);

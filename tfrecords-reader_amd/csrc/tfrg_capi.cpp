@@ -67,6 +67,9 @@ struct tfrg_ctx {
   hipStream_t last_stream = nullptr;
   uint32_t lane_max = 2048;
   uint32_t wave_stage = 0xffffffffu;  // clamped to the kernel's stage size
+  uint64_t record_bound = 0;  // tfrg_ctx_set_record_bound: no record above this (0 = unknown)
+  bool stage_count = false;   // tfrg_ctx_set_stage_count (env TFRG_STAGE_COUNT)
+  uint64_t call_bound = 0;    // tfrg_decode_host: the bound of its own ranges (one call)
   int num_cus = 256;
   // constants
   DBuf crc_tab, consts;
@@ -121,6 +124,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
+  if (const char* e = getenv("TFRG_STAGE_COUNT")) c->stage_count = atoi(e) != 0;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -131,7 +135,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
   // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
   // 32 round shifts x^(8192 * 2^k)
-  std::vector<uint32_t> tab(8192 + 16384 + 2048 + 24 * 1024), cst(128);
+  std::vector<uint32_t> tab(8192 + 16384 + 2048 + 24 * 1024), cst(256);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -157,6 +161,9 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts
+  // k_stage_count: lane l's CRC slice ends 196 (63 - l) bytes before the padded payload end
+  for (int l = 0; l < 64; ++l) cst[128 + l] = gf_xpow8(196ull * (63 - l));
+  for (int l = 0; l < 64; ++l) cst[192 + l] = gf_xpow8(196ull * (63 - l) + 96);  // (its first 100 bytes)
   if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||
       hipMemcpy(c->crc_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->consts.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -189,6 +196,18 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
 int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
   if (!c) return TFRG_E_ARG;
   c->lane_max = lane_max;
+  return 0;
+}
+
+int tfrg_ctx_set_stage_count(tfrg_ctx* c, int on) {
+  if (!c) return TFRG_E_ARG;
+  c->stage_count = on != 0;
+  return 0;
+}
+
+int tfrg_ctx_set_record_bound(tfrg_ctx* c, uint64_t max_record_bytes) {
+  if (!c) return TFRG_E_ARG;
+  c->record_bound = max_record_bytes;
   return 0;
 }
 
@@ -658,6 +677,10 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
   cfg.lane_max = c->lane_max;
   cfg.wave_stage = c->wave_stage;
+  // k_stage_count only when a record above lane_max may exist (its empty launch costs microseconds)
+  const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
+  c->call_bound = 0;
+  cfg.stage_count = c->stage_count && (bound == 0 || bound > c->lane_max);
   if (n) {
     hipEvent_t* ev = nullptr;
     if (c->profiling) {
@@ -724,12 +747,14 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
     HIP_TRY(hipMemcpyAsync(c->in_start.p, h_start, (size_t)n * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(c->in_end.p, h_end, (size_t)n * 8, hipMemcpyHostToDevice, st));
   }
-  uint64_t total = 0;  // bytes of all ranges (clamped to the buffer): repeated ranges count again
+  uint64_t total = 0, widest = 0;  // bytes of all ranges (clamped to the buffer): repeated ranges count again
   for (uint32_t i = 0; i < n; ++i) {
     const uint64_t a = h_start[i], b = h_end[i] < nbytes ? h_end[i] : nbytes;
     if (b > a) total += b - a;
+    if (h_end[i] > a && h_end[i] - a > widest) widest = h_end[i] - a;
   }
   c->cap_hint = total;
+  c->call_bound = widest ? widest : 1;
   if (!c->tpl_learned && c->n_keys && c->tpl_on) {  // record shapes of the first host batch of a schema
     const int t = tfrg_learn_templates(c, h_bytes, nbytes, h_start, h_end, n, flags);
     if (t < 0) return t;

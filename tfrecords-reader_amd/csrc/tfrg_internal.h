@@ -185,11 +185,12 @@ struct LaunchCfg {
   int wave_grid;
   uint32_t lane_max;       // records above this size go to the wave kernels
   uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
+  bool stage_count;        // the batch may hold staged records above lane_max: launch k_stage_count
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageTailCount, kStageSpine, kStageDownGather, kStageTailGather,
-                   kStageMaterialize, kNumStages };
+enum Stage : int { kStageLaneCount = 0, kStageStageCount, kStageTailCount, kStageSpine, kStageDownGather,
+                   kStageTailGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

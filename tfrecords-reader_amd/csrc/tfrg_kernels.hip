@@ -1495,7 +1495,8 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 template <int R, bool COMPAT, int MODE>
 __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
-                                                                           uint32_t lane_max, uint32_t wave_stage) {
+                                                                           uint32_t lane_max, uint32_t wave_stage,
+                                                                           uint32_t stage_cnt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // slicing tables at a static LDS address: lookups fold the table base into the ds_read offset
   __shared__ uint32_t tab[256 * kLaneSlice * R];
@@ -1551,6 +1552,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     }
     RecView v{};
     bool mine = false;
+    bool stg = false;  // counted by k_stage_count (staged large record, launched for this batch)
     if (valid) {
       v = rec_view_se(B, cst0, cen0);
       const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
@@ -1558,6 +1560,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
         if (v.e - (v.st & ~15ull) <= wave_stage) {
           const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
           o.big_list[i] = r;
+          stg = stage_cnt != 0u;
         } else {
           const uint32_t i = atomicAdd(&o.info[kInfoHuge], 1u);
           o.big_list[B.n - 1u - i] = r;
@@ -1616,7 +1619,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     // canonical walk straight from HBM, one record per lane (64 latency chains in flight per wave).
     // The payload CRC of records above lane_max is k_big_crc's streaming pass; the others' is
     // computed here, serially per lane from HBM.
-    const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));
+    const bool bigw = fast_ok && valid && ((!mine && !stg) || (span_rec && !staged));
     if (__ballot(bigw)) {
       if (bigw) {
         // (the payload CRC of a large record is role 2's stream, unless it is shorter than one round)
@@ -1632,7 +1635,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     }
     PHASE_MARK(p4);
     // everything else of this wave's records goes to the exact walker
-    const bool slow = valid && !done;
+    const bool slow = valid && !done && !stg;
     const uint64_t sm = __ballot(slow);
     if (sm) {
       uint32_t b0 = 0;
@@ -1682,7 +1685,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       }
       if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
         if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
-        const uint64_t irm = __ballot(valid && !(done && c == (1u | kCountInline)));
+        const uint64_t irm = __ballot(valid && !stg && !(done && c == (1u | kCountInline)));
         if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
       }
     }
@@ -2358,7 +2361,7 @@ struct Pref {  // named fields, returned by value: an array or an out-parameter 
 #define TFRG_PREF_LOAD(j)                                                        \
   {                                                                              \
     const uint64_t q = lo16 + lane * 16u + (uint32_t)(j)*1024u;                  \
-    p.w##j = *reinterpret_cast<const uint4*>(src + (q < hi ? q : 0ull));          \
+    p.w##j = *reinterpret_cast<const uint4*>(src + (q < hi ? q : lo16c));         \
   }
 #define TFRG_PREF_STORE(j)                                                       \
   {                                                                              \
@@ -2367,6 +2370,9 @@ struct Pref {  // named fields, returned by value: an array or an out-parameter 
   }
 
 __device__ __forceinline__ Pref pref_load_v(const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  // the loads past the record re-read its first 16 bytes (one line, already requested): clamping
+  // them to the batch start put every wave's spare loads on the same few lines of one L2 channel
+  const uint64_t lo16c = hi > lo16 ? lo16 : 0ull;
   Pref p;
   static_assert(kPrefWords <= 12 && kWStage % 1024 == 0, "pref_load is spelled out for up to 12 words");
   TFRG_PREF_LOAD(0) TFRG_PREF_LOAD(1) TFRG_PREF_LOAD(2) TFRG_PREF_LOAD(3) TFRG_PREF_LOAD(4) TFRG_PREF_LOAD(5)
@@ -2381,6 +2387,415 @@ __device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t
 }
 #undef TFRG_PREF_LOAD
 #undef TFRG_PREF_STORE
+
+// ------------------------------------------------------------------------------------------------
+// Records above lane_max whose span fits the stage (big_list[0, kInfoBig)): the count pass, one WAVE
+// per record, from ONE LDS copy of the record (k_stage_count, launched between k_lane_count and
+// k_tail_count when the batch may hold such records and the schema has <= 64 slots).
+//  * framing: the length field and the masked CRC-32C of its 8 bytes;
+//  * the payload CRC-32C, lane-parallel from the stage: lane l owns the 49 aligned words ending
+//    196 (63 - l) bytes before the payload's word-padded end (kSgQ x 64 >= the 12 KiB stage), a
+//    slice-by-8 chain from a zero state over them (the payload's first 4 bytes inverted: the ~0
+//    initial state, crc32c.h), placed by x^(8 * 196 (63 - l)) (gf_mul) and XOR-reduced over the
+//    wave; the z <= 3 zero bytes padding the last word are matched by advancing the stored CRC's
+//    state over z zero bytes (as role_crc_stream's flush);
+//  * fast_walk's canonical walk, ENTRY-PARALLEL: all lanes scan the Features body for entry starts
+//    (0x0a tag, 1- or 2-byte length, the key's 0x0a tag: every canonical entry, a few false
+//    positives), the candidates are compacted in position order and each is parsed by its own
+//    lane with fast_walk's per-entry checks; the parsed entries must chain from the body's start to
+//    its end (a false candidate surviving the checks, or a non-canonical record -> the exact
+//    walker), their chain positions are the ranks;
+//  * the dict (order / count / loc words, inline single values, speculative placement) and the
+//    tile sums, one slot per lane.
+// For these records it replaces the lane kernel's per-lane walk from HBM (one dependent HBM round
+// trip per entry header: C3's count pass was latency-bound at 1.9 TB/s) and their entry in the
+// streaming-CRC list (a second read of every payload).
+constexpr uint32_t kSgMaxSlots = 64;                 // one slot per lane
+constexpr uint32_t kSgCandCap = 1024;                // entry candidates per record
+// payload bytes per lane for the CRC: 49 words, an odd word stride between lanes, so the data reads
+// of a 32-lane group hit 32 different banks (48 words put every other lane on the same bank)
+constexpr uint32_t kSgQ = 196;
+constexpr uint32_t kCstStageLane = 128;              // consts [128, 192): x^(8 * kSgQ * (63 - l)),
+                                                     // [192, 256): x^(8 * (kSgQ * (63 - l) + 96))
+constexpr uint32_t kSgRegion = (kWStageStride + 2u * kSgCandCap + 64u * 16u + 32u + 15u) & ~15u;
+static_assert(kSgQ * 64 >= kWStage && kSgQ % 4 == 0 && (kSgQ / 4) % 2 == 1, "lane CRC slices");
+
+// bit 7 of every byte of x that is zero, exactly (no borrow from a lower byte)
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
+  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
+}
+
+// word y of the payload [a, b) (stage offsets): bytes outside zeroed, bytes [a, a + 4) inverted
+__device__ __forceinline__ uint32_t sg_mask_word(uint32_t w, uint32_t y, uint32_t a, uint32_t b) {
+  auto below = [](uint32_t x, uint32_t y_) {  // bytes of the word at y_ below x
+    return x <= y_ ? 0u : (x - y_ >= 4u ? 0xffffffffu : (1u << ((x - y_) << 3)) - 1u);
+  };
+  const uint32_t ba = below(a, y), keep = below(b, y) & ~ba, inv = below(a + 4u, y) & ~ba & keep;
+  return (w & keep) ^ inv;
+}
+
+// masked CRC-32C of the payload at stage [a, b) equals `stored` (L = b - a >= 256). Each lane's
+// 49 words run as two independent chains (its first 25 words and its last 24: twice the LDS
+// round trips in flight), placed by x^(8 (196 (63 - l) + 96)) and x^(8 * 196 (63 - l)).
+__device__ __forceinline__ bool sg_payload_crc(const uint8_t* l, uint32_t a, uint32_t b, uint32_t stored,
+                                               const LdsTab<1>& T, uint32_t Kl, uint32_t KlA, uint32_t lane) {
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(l);
+  const uint32_t bw = (b + 3u) & ~3u, z = bw - b;
+  const uint32_t back = kSgQ * (63u - lane);  // bytes between this lane's words and bw
+  const uint32_t a4 = a & ~3u;
+  uint32_t S = 0;
+  if (bw > back + a4) {  // some payload byte in this lane's words
+    const uint32_t x1 = bw - back;
+    // words below a4 (masked to zero: a zero state stays zero) may precede the payload: a framed
+    // payload starts at stage offset >= 12, so x1 - 196 >= 0 unless this lane holds the start;
+    // there the chains begin at the first pair holding a4 - 4 or later
+    // (signed: the slice of the lane holding the payload start may begin before the stage; only
+    // words at or above a4 - 4 >= 8 are read)
+    const int32_t yA = (int32_t)x1 - (int32_t)kSgQ, yB = (int32_t)x1 - 96, ia4 = (int32_t)a4;
+    auto word = [&](int32_t y) {
+      const uint32_t w = W[y >> 2];
+      return ((uint32_t)y < a + 4u || (uint32_t)y + 4u > b) ? sg_mask_word(w, (uint32_t)y, a, b) : w;
+    };
+    uint32_t SA = yA + 4 > ia4 ? T.step4(word(yA)) : 0u, SB = 0u;  // chain A: 1 + 12 pairs
+#pragma unroll 2
+    for (int32_t k = 0; k < 12; ++k) {
+      const int32_t ya = yA + 4 + 8 * k, yb = yB + 8 * k;
+      if (ya + 8 > ia4) SA = T.step8(SA ^ word(ya), word(ya + 4));
+      if (yb + 8 > ia4) SB = T.step8(SB ^ word(yb), word(yb + 4));
+    }
+    S = gf_mul(SA, KlA) ^ gf_mul(SB, Kl);
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) S ^= (uint32_t)__shfl_xor((int)S, m, 64);
+  const uint32_t um = stored - kCrcMaskDelta;
+  uint32_t v = ~((um << 15) | (um >> 17));  // ~crc_mask^-1(stored) = U(~0, payload) un-inverted
+  for (uint32_t k = 0; k < z; ++k) v = (v >> 8) ^ T(0u, v & 0xffu);
+  return v == S;
+}
+
+// bit 7 of the 16 bytes of a block, byte i -> bit i
+__device__ __forceinline__ uint32_t cont16(uint4 b) {
+  auto nib = [](uint32_t w) {
+    w = (w >> 7) & 0x01010101u;
+    return (w | (w >> 7) | (w >> 14) | (w >> 21)) & 0xfu;
+  };
+  return nib(b.x) | (nib(b.y) << 4) | (nib(b.z) << 8) | (nib(b.w) << 12);
+}
+
+// count_packed over the LDS stage, one aligned 16-byte block per step (one ds_read_b128) and the
+// block's 16 continuation bits at once: terminators = popcount, the run of continuation bytes
+// carried across blocks checked at the first terminator, runs of >= 10 after a terminator found by
+// a 10-fold AND of shifts. Same verdicts as count_packed (a varint of > 10 bytes, or a chunk not
+// ending on a terminator, bails), without its byte-serial dependency chain.
+__device__ __forceinline__ bool count_packed16(const FastSrc& s, uint32_t o, uint32_t e, uint32_t& cnt) {
+  uint32_t run = 0, terms = 0;
+  bool bad = false;
+  const uint32_t a0 = s.p + o, a1 = s.p + e;
+  for (uint32_t q = a0 & ~15u; q < a1; q += 16u) {
+    const uint4 blk = *reinterpret_cast<const uint4*>(s.l + q);
+    const uint32_t lo = a0 > q ? a0 - q : 0u, hi = a1 - q < 16u ? a1 - q : 16u;  // valid bytes [lo, hi)
+    const uint32_t valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+    const uint32_t m = cont16(blk), t = ~m & valid, cm = m & valid;
+    const uint32_t a = cm & (cm >> 1), b = a & (a >> 2), c = b & (b >> 4);
+    bad |= ((c & (a >> 8)) & (t << 1)) != 0u;  // >= 10 continuation bytes right after a terminator
+    if (!t) {
+      run += hi - lo;
+    } else {
+      bad |= run + (uint32_t)__builtin_ctz(t) - lo >= 10u;  // the run carried in, ended here
+      run = hi - 1u - (31u - (uint32_t)__builtin_clz(t));
+      terms += (uint32_t)__popc(t);
+    }
+    bad |= run >= 10u;
+  }
+  if (bad || (e > o && run)) return false;  // the last varint runs past the chunk
+  cnt = terms;
+  return true;
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(kWaveBlock, 2) void k_stage_count(DevBatch B, DevSchema sc, DevOut o,
+                                                               const uint32_t* __restrict__ crc_tab,
+                                                               const uint32_t* __restrict__ consts) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  const uint32_t nbig = o.info[kInfoBig];
+  if (blockIdx.x * kWavesPerBlock >= nbig) return;  // block-uniform
+  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint32_t* tab = lds;  // [8][256] slice-by-8
+  uint32_t* kht = lds + 2048;
+  uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
+  uint8_t* region = reinterpret_cast<uint8_t*>(krec + sc.n_keys * kKrWords) + wib * kSgRegion;
+  uint8_t* stage = region;
+  uint16_t* cand = reinterpret_cast<uint16_t*>(region + kWStageStride);
+  uint32_t* d_ord = reinterpret_cast<uint32_t*>(cand + kSgCandCap);
+  uint32_t* d_cw = d_ord + 64;
+  uint2* d_lv = reinterpret_cast<uint2*>(d_cw + 64);
+  uint32_t* seen = reinterpret_cast<uint32_t*>(d_lv + 64);
+  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) tab[i] = crc_tab[2048 + i];
+  for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
+  for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
+  __syncthreads();
+  const LdsTab<1> T{tab, 0};
+  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
+  const uint32_t S = sc.n_slots;
+  const uint32_t Kl = consts[kCstStageLane + lane], KlA = consts[kCstStageLane + 64 + lane];
+  const uint32_t spec_k = (sc.spec && lane < S) ? sc.spec[lane] : 0u;
+  const bool framed = !(B.flags & kFlagPayloadOnly), do_crc = framed && !(B.flags & kFlagNoCrc);
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(stage);
+
+  const uint32_t stride = gridDim.x * kWavesPerBlock;
+  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
+  if (i >= nbig) return;  // wave-uniform (no block barrier below)
+  // three-stage record queue, as role_stage_gather: the next record's bytes in registers while this
+  // one is counted from the stage
+  RecPipe q;
+  q.r1 = o.big_list[i];
+  q.s1 = B.start[q.r1];
+  q.e1 = B.end[q.r1];
+  Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
+  q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
+  q.s2v = B.start[vgpr_launder(q.r2)];
+  q.e2v = B.end[vgpr_launder(q.r2)];
+  q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
+  for (; i < nbig; i += stride) {
+    PHASE_MARK(t0);
+    const uint32_t r = q.r1;
+    const RecView v = rec_view_se(B, q.s1, q.e1);
+    const uint64_t lo16 = v.st & ~15ull;
+    pref_store(pf, stage, lo16, v.e, lane);
+    if (lane < 64u) {
+      d_ord[lane] = 0u;
+      if (lane < 8u) seen[lane] = 0u;
+    }
+    wave_lds_sync();
+    q.r1 = q.r2;
+    q.s1 = rfl64(q.s2v);
+    q.e1 = rfl64(q.e2v);
+    q.r2 = rfl32(q.r3v);
+    q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
+    if (i + stride < nbig) pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
+    q.s2v = B.start[vgpr_launder(q.r2)];
+    q.e2v = B.end[vgpr_launder(q.r2)];
+    PHASE_MARK(t1);
+    PHASE_ADD(0, t0, t1);
+
+#ifdef TFRG_SG_ONLY_STAGE
+    if (lane == 0) o.verdict[r] = (uint8_t)W[lane];
+    wave_lds_sync();
+    continue;
+#endif
+    // ---- framing verdicts (frame_verdicts' conditions)
+    uint32_t verdict = v.verdict;
+    const uint32_t so = (uint32_t)(v.st - lo16), pa = (uint32_t)(v.p0 - lo16), L = (uint32_t)v.L;
+    const uint64_t D = v.e - v.st;
+    if (framed && D >= 8) {
+      const uint32_t lw0 = lds_u32u(stage, so), lw1 = lds_u32u(stage, so + 4u);
+      if ((((uint64_t)lw1 << 32) | lw0) == v.en - v.st - 16) verdict |= TFRG_V_LEN_MATCH;
+      if (do_crc && D >= 12) {
+        const uint32_t c = ~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1);
+        if (crc_mask(c) == lds_u32u(stage, so + 8u)) verdict |= TFRG_V_LEN_CRC;
+      }
+      if (do_crc && D >= 16) {
+        const uint32_t stored = lds_u32u(stage, pa + L);
+        const bool okc = L >= 256u ? sg_payload_crc(stage, pa, pa + L, stored, T, Kl, KlA, lane)
+                                   : crc_mask(crc_lds8<1>(stage, pa, pa + L, T)) == stored;
+        if (okc) verdict |= TFRG_V_DATA_CRC;
+      }
+    }
+
+    PHASE_MARK(t2);
+    PHASE_ADD(1, t1, t2);
+#ifdef TFRG_SG_NO_PARSE
+    if (lane == 0) o.verdict[r] = (uint8_t)verdict;
+    wave_lds_sync();
+    continue;
+#endif
+    // ---- entry-parallel canonical walk
+    const FastSrc fs{stage, pa, L, v.p0};
+    uint32_t fn, fo, fl;
+    bool good = hdr2(fs, 0, L, fn, fo, fl) & (fn == 1u) & (fo + fl == L);
+    const uint32_t fe = fo + fl;
+    // entry-start candidates of the body, 256 bytes per step (lane j: aligned word j, so the reads
+    // are bank-conflict-free): position p (stage offset) holding 0x0a, then a 1-byte length and
+    // 0x0a, or a 2-byte length and 0x0a; numbered across the wave in position order
+    const uint32_t ba = pa + fo, be = pa + fe;
+    uint32_t total = 0;
+    if (good) {
+      const uint64_t lt = (1ull << lane) - 1ull;
+      for (uint32_t row = ba & ~15u; row < be; row += 1024u) {  // (wave-uniform)
+        const uint32_t y = row + 16u * lane;
+        uint4 blk = make_uint4(0, 0, 0, 0);
+        if (y < be) blk = *reinterpret_cast<const uint4*>(stage + y);
+        uint32_t nxt = (uint32_t)__shfl_down((int)blk.x, 1, 64);  // the next block's first word
+        if (lane == 63u && y + 16u < be) nxt = W[(y + 16u) >> 2];
+        const uint32_t ws[5] = {blk.x, blk.y, blk.z, blk.w, nxt};
+        uint32_t c16 = 0;  // candidate bits: bit 4k + j = position y + 4k + j
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t w = ws[k], wn = ws[k + 1];
+          const uint32_t w1 = __builtin_amdgcn_alignbyte(wn, w, 1u), w2 = __builtin_amdgcn_alignbyte(wn, w, 2u);
+          const uint32_t w3 = __builtin_amdgcn_alignbyte(wn, w, 3u);
+          const uint32_t e0 = zero_bytes(w ^ 0x0a0a0a0au), e2 = zero_bytes(w2 ^ 0x0a0a0a0au);
+          const uint32_t e3 = zero_bytes(w3 ^ 0x0a0a0a0au);
+          const uint32_t h1 = w1 & 0x80808080u, h2 = w2 & 0x80808080u;
+          const uint32_t c = (e0 & ((~h1 & e2) | (h1 & ~h2 & e3))) >> 7;  // bit 8 j: position 4k + j
+          c16 |= ((c | (c >> 7) | (c >> 14) | (c >> 21)) & 0xfu) << (4 * k);
+        }
+        // positions inside the body
+        const uint32_t lo = ba > y ? (ba - y < 16u ? ba - y : 16u) : 0u, hi = be > y ? (be - y < 16u ? be - y : 16u) : 0u;
+        c16 &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+        const uint32_t nc = (uint32_t)__popc(c16);
+        const uint64_t b0 = __ballot(nc & 1u), b1 = __ballot(nc & 2u), b2 = __ballot(nc & 4u);
+        const uint64_t b3 = __ballot(nc & 8u), b4 = __ballot(nc & 16u);
+        uint32_t at = total + (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) +
+                      4u * (uint32_t)__popcll(b2 & lt) + 8u * (uint32_t)__popcll(b3 & lt) +
+                      16u * (uint32_t)__popcll(b4 & lt);
+        while (c16) {
+          if (at < kSgCandCap) cand[at] = (uint16_t)(y + (uint32_t)__builtin_ctz(c16));
+          ++at;
+          c16 &= c16 - 1u;
+        }
+        total += (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2) +
+                 8u * (uint32_t)__popcll(b3) + 16u * (uint32_t)__popcll(b4);
+      }
+    }
+    good &= total <= kSgCandCap;
+    wave_lds_sync();
+#ifdef TFRG_SG_SCAN_ONLY
+    if (lane == 0) o.verdict[r] = (uint8_t)(verdict + total);
+    wave_lds_sync();
+    continue;
+#endif
+    PHASE_MARK(t3);
+    PHASE_ADD(3, t2, t3);
+    uint32_t chain = fo, rank0 = 0;  // payload offset the next entry must start at; entries so far
+    for (uint32_t w0 = 0; good && w0 < total; w0 += 64u) {  // (wave-uniform)
+      const uint32_t ci = w0 + lane;
+      const bool has = ci < total;
+      const uint32_t qp = has ? (uint32_t)cand[ci] - pa : fo;  // payload offset of the candidate
+      uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
+      bool pat = has & hdr2(fs, qp, fe, en, eo, el) & (en == 1u);
+      const uint32_t ee = eo + el;
+      pat &= hdr2(fs, eo, ee, kn, ko, kl) & (kn == 1u);
+      pat &= hdr2(fs, ko + kl, ee, vn, vo, vl) & (vn == 2u) & (vo + vl == ee);
+      pat &= hdr2(fs, vo, ee, kind, lo, ll) & (lo + ll == ee) & (kind - 1u < 3u);
+      // the surviving candidates must chain: each starts where the previous one ends
+      const uint64_t pm = __ballot(pat);
+      const uint64_t below = pm & ((1ull << lane) - 1ull);
+      const int pl = below ? 63 - __builtin_clzll(below) : 0;
+      const uint32_t pend = (uint32_t)__shfl((int)ee, pl, 64);
+      const uint32_t want = below ? pend : chain;
+      good &= !__ballot(pat && qp != want);
+      if (!good) break;
+      const uint32_t rank = rank0 + (uint32_t)__popcll(below) + 1u;
+      bool eok = true;
+      if (pat) {
+        const int kid = fast_lookup(fs, K, ko, kl);
+        uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0, c0w = 0;
+        const uint32_t le = lo + ll;
+        for (uint32_t g = lo; eok && g < le;) {
+          uint32_t cf, co, cl;
+          eok = hdr2(fs, g, le, cf, co, cl) & (cf == 1u);
+          g = co + cl;
+          if (kind == TFRG_KIND_BYTES) {
+            ++cnt;
+          } else if (kind == TFRG_KIND_FLOAT) {
+            eok &= (cl & 3u) == 0u;
+            cnt += cl >> 2;
+          } else if (cl <= 4u) {
+            const uint32_t m = bytes_mask(cl);
+            const uint32_t wv = fs.u32(co) & m;
+            const uint32_t tm = ~wv & 0x80808080u & m;
+            eok &= cl == 0u || ((tm >> ((cl << 3) - 1u)) & 1u);
+            cnt += __popc(tm);
+            if (nch == 0) c0w = wv;
+          } else {
+            uint32_t kk = 0;
+#ifndef TFRG_SG_NO_COUNT
+            eok &= count_packed16(fs, co, co + cl, kk);
+#else
+            kk = cl >> 2;
+#endif
+            cnt += kk;
+          }
+          if (nch == 0) {
+            c0o = co;
+            c0l = cl;
+          }
+          ++nch;
+        }
+        eok &= kid >= 0;
+        int slot = -1;
+        if (eok) {
+          slot = (int)K.rec[(uint32_t)kid * kKrWords + kKrSlot1 + kind - 1u];
+          const uint32_t bit = 1u << ((uint32_t)kid & 31u);
+          const uint32_t old = atomicOr(&seen[(uint32_t)kid >> 5], bit);  // a duplicate key bails
+          eok &= !(old & bit) & (slot >= 0) & (rank < 65534u);
+        }
+        if (eok) {
+          uint2 lv = make_uint2(lo, ll);
+          uint32_t cw = cnt;
+          if (cnt == 1u && nch == 1u) {
+            if (kind == TFRG_KIND_BYTES) {
+              lv = make_uint2((uint32_t)(fs.base + c0o), c0l);
+              cw = 1u | kCountInline;
+            } else if (kind == TFRG_KIND_FLOAT) {
+              lv = make_uint2(fs.u32(c0o), 0u);
+              cw = 1u | kCountInline;
+            } else if (c0l <= 4u) {
+              lv = make_uint2(vgroups(c0w, 0xffffffffu), 0u);
+              cw = 1u | kCountInline;
+            }
+          }
+          d_ord[slot] = rank;
+          d_cw[slot] = cw;
+          d_lv[slot] = lv;
+        }
+      }
+      good &= !__ballot(pat && !eok);
+      if (pm) chain = __builtin_amdgcn_readlane(ee, 63 - __builtin_clzll(pm));
+      rank0 += (uint32_t)__popcll(pm);
+    }
+    good &= chain == fe;
+    wave_lds_sync();
+    PHASE_MARK(t4);
+    PHASE_ADD(4, t3, t4);
+
+    // ---- results
+    if (!good || !strict_pass(B, verdict, true)) {  // the exact walker (k_tail_count role 1)
+      if (lane == 0) {
+        const uint32_t si = atomicAdd(&o.info[kInfoSlow], 1u);
+        o.slow_list[si] = r;
+        o.verdict[r] = (uint8_t)kVerdictPending;
+      }
+      if (spec_k) atomicAdd(&o.irr[lane], 1u);
+    } else {
+      if (lane == 0) {
+        o.status[r] = TFRG_OK;
+        o.verdict[r] = (uint8_t)verdict;
+      }
+      if (lane < S) {
+        const uint32_t ov = d_ord[lane];
+        const uint32_t cw = ov ? d_cw[lane] : 0u;
+        const size_t at = (size_t)lane * B.n + r;
+        o.order[at] = (uint16_t)ov;
+        o.count[at] = cw;
+        if (ov) {
+          const uint2 lv = d_lv[lane];
+          if (spec_k && (cw & kCountInline)) put_inline(o, spec_k & 3u, lv, (uint64_t)B.n * ((spec_k >> 2) - 1u) + r);
+          else o.loc[at] = lv;
+        }
+#ifndef TFRG_SG_NO_TSUM
+        if (cw & ~kCountInline) atomicAdd(&o.tsum[(size_t)lane * o.tile_stride + (r >> kTileShift)], cw & ~kCountInline);
+#endif
+        if (spec_k && cw != (1u | kCountInline)) atomicAdd(&o.irr[lane], 1u);
+      }
+    }
+    wave_lds_sync();  // (the stage and the dict are rewritten by the next record)
+    PHASE_MARK(t5);
+    PHASE_ADD(6, t4, t5);
+    PHASE_ADD(7, t0, t5);
+  }
+}
 
 // ------------------------------------------------------------------------------------------------
 // Row-split scan, second level: the tile sums of every slot in chunks of 4096 tiles (1 M records),
@@ -3295,7 +3710,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 
 constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_tail_count",  "k_spine",
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_stage_count", "k_tail_count", "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -3320,6 +3735,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   DevSchema scx = sc;
   if (lane_lds > kLaneLdsBudget || !fast_ok) scx.spec = nullptr;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
+  // staged large records counted by k_stage_count (else the lane kernel walks them from HBM)
+  const uint32_t sg = cfg.stage_count && fast_ok && S <= kSgMaxSlots ? 1u : 0u;
 
   mark(kStageLaneCount);
   // one round of resident workgroups (a second, partial round would idle most CUs at the tail)
@@ -3333,17 +3750,27 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
-                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
+                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
   } else if (S <= 64) {
     const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
-                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
   } else {
     const size_t lds = stage_lds + keys_lds + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
-                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
+  }
+  mark(kStageStageCount);
+  if (sg) {  // one round of resident workgroups over the staged large records
+    const size_t lds = 2048 * 4 + keys_lds + (size_t)kSgRegion * kWavesPerBlock;
+    const void* fn = reinterpret_cast<const void*>(&k_stage_count<COMPAT>);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
+      per_cu = 1;
+    const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
+    hipLaunchKernelGGL((k_stage_count<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, d_tab, d_consts);
   }
   mark(kStageTailCount);
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits

@@ -2,6 +2,11 @@
 
 The library is built in-tree (``tfrecords-reader_amd/csrc/Makefile`` -> ``tfr_reader/libtfrg.so``).
 There is no fallback: if the library cannot be loaded every decode entry point raises.
+
+A process that also uses torch (ROCm build) should import torch first: libtfrg then binds to the HIP
+runtime torch bundles (same soname, libamdhip64.so.7). Loaded before torch, it brings in
+/opt/rocm's runtime and torch later loads its own copy beside it: two HIP / HSA runtimes in one
+process, and torch's finds no device.
 """
 
 from __future__ import annotations
@@ -76,6 +81,8 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_ctx_destroy": (C.c_int, [C.c_void_p]),
     "tfrg_ctx_set_lane_max": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_wave_stage": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "tfrg_ctx_set_record_bound": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "tfrg_ctx_set_stage_count": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_learn_templates": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_uint32]),
     "tfrg_template_count": (C.c_int, [C.c_void_p]),

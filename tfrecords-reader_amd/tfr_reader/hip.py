@@ -133,6 +133,15 @@ class HipDecoder:
         N.check(min(k, 0), "tfrg_learn_templates")
         return int(k)
 
+    def set_stage_count(self, on: bool) -> None:
+        """Count large staged records with k_stage_count (tfrg_ctx_set_stage_count; off by default)."""
+        N.check(self._lib.tfrg_ctx_set_stage_count(self._ctx, int(bool(on))), "tfrg_ctx_set_stage_count")
+
+    def set_record_bound(self, nbytes: int) -> None:
+        """Upper bound on (end - start) of the records of later ``decode_device`` calls (0 = unknown):
+        a bound <= lane_max skips the large-record count launch (tfrg_ctx_set_record_bound)."""
+        N.check(self._lib.tfrg_ctx_set_record_bound(self._ctx, int(nbytes)), "tfrg_ctx_set_record_bound")
+
     def set_wave_stage(self, nbytes: int) -> None:
         """Records above lane_max spanning <= nbytes go to the LDS-staged wavefront kernels."""
         N.check(self._lib.tfrg_ctx_set_wave_stage(self._ctx, nbytes), "tfrg_ctx_set_wave_stage")

@@ -261,11 +261,16 @@ class ShardDecoder:
             d.push_schema()
             d.learn_templates(buf[lo:hi], st - np.uint64(lo), en - np.uint64(lo))
 
-    def decode_device(self, plan: np.ndarray, d_bytes: int, d_start: int, d_end: int, streams=None, **kw) -> None:
+    def decode_device(self, plan: np.ndarray, d_bytes: int, d_start: int, d_end: int, streams=None,
+                      max_record: int | None = None, **kw) -> None:
         """Enqueue every batch of a device-resident shard: image at d_bytes (readable to its 16-byte
         round-up), d_start / d_end the ``rebase``d offsets (u64 device arrays). Batch k runs on
-        ``streams[k % len(streams)]`` (HIP stream handles; default: each context's own stream)."""
+        ``streams[k % len(streams)]`` (HIP stream handles; default: each context's own stream).
+        ``max_record``: an upper bound on end - start (HipDecoder.set_record_bound), if known."""
         decs = self._decoders(len(plan))
+        if max_record is not None:
+            for d in decs:
+                d.set_record_bound(max_record)
         for k, (r0, r1, lo, hi) in enumerate(plan.tolist()):
             s = streams[k % len(streams)] if streams else None
             decs[k].decode_device(d_bytes + lo, hi - lo, d_start + 8 * r0, d_end + 8 * r0, r1 - r0, stream=s, **kw)

@@ -67,7 +67,7 @@ def main():
         L = _native.lib()
         arr = (ctypes.c_ulonglong * 32)()
         L.tfrg_debug_phase(arr, 32, 1)
-        names = ["c.stage", "c.crc", "-", "c.phaseA", "c.phaseB", "-", "c.final", "c.total",
+        names = ["sg.stage", "sg.crc", "-", "sg.scan", "sg.parse", "-", "sg.out", "sg.total",
                  "c.bails", "g.stage+meta", "g.groups", "g.int64", "g.lane", "h.crc", "h.walk", "g.float",
                  "l.span+stage", "l.crc", "l.walk", "l.final", "l.total", "s.search", "s.load+chunk",
                  "s.horner+flush", "-", "s.total", "s.batches"]
