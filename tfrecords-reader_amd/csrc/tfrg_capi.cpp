@@ -498,6 +498,25 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
     memcpy(d + kTplBytes, x.bytes.data(), x.L);
     memcpy(d + kTplMask, x.mask.data(), x.L);
     memcpy(d + kTplEnt, x.ent.data(), x.ent.size() * 4);
+    d[kTplV0] = 0xffffffffu;
+    if (x.L >= 4) {  // the CRC shortcut of a matching record (tfrg_internal.h)
+      static CrcTables CT;
+      static bool ct_made = false;
+      if (!ct_made) {
+        crc_make_tables(&CT);
+        ct_made = true;
+      }
+      std::vector<uint8_t> f(x.L);
+      uint32_t v0 = x.L;
+      for (uint32_t i = 0; i < x.L; ++i) {
+        f[i] = (uint8_t)(x.bytes[i] & x.mask[i]) ^ (i < 4 ? 0xffu : 0u);
+        if (x.mask[i] != 0xffu && v0 == x.L) v0 = i;
+      }
+      const uint64_t L64 = x.L;
+      d[kTplCrcK] = crc_update_bytes(CT, 0u, f.data(), x.L);
+      d[kTplLenCrc] = tfrg_masked_crc32c(reinterpret_cast<const uint8_t*>(&L64), 8);
+      d[kTplV0] = v0;
+    }
   }
   HIP_TRY(hipSetDevice(c->device));
   if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));

@@ -38,8 +38,13 @@ struct DevSchema {
 // [4, 4+64) bytes, [68, 68+64) mask, [132, 132+4*16) entries {slot | mode << 24, rank, count word,
 // a | b << 16}; mode 0: loc (a, b) = (list offset, list length), 1: inline int64 varint at a of b
 // bytes, 2: inline float at a, 3: inline bytes element at a of b bytes.
+// [196] K = U(0, (bytes & mask) with its first 4 bytes inverted) over the L bytes, [197] the masked
+// CRC-32C of the 8 length bytes of L, [198] v0 = the first payload byte with a variable bit
+// (0xffffffff: no CRC shortcut, L < 4). A matching record M = (bytes & mask) ^ V, V = M & ~mask, so
+// its CRC-32C is ~(K ^ U(0, V[v0, L))) (U linear, crc32c.h): only the bytes from v0 on are read.
 constexpr uint32_t kTplMaxL = 256, kTplMaxEntries = 16, kTplMax = 4;
-constexpr uint32_t kTplBytes = 4, kTplMask = 68, kTplEnt = 132, kTplWords = 196;
+constexpr uint32_t kTplBytes = 4, kTplMask = 68, kTplEnt = 132, kTplCrcK = 196, kTplLenCrc = 197, kTplV0 = 198,
+                   kTplWords = 200;
 
 // Packed per-key record (8 x u32) staged into LDS by the lane kernels' fast path.
 enum KeyRec : uint32_t { kKrHash = 0, kKrLen, kKrW0, kKrW1, kKrSlot1, kKrSlot2, kKrSlot3, kKrFlags, kKrWords };

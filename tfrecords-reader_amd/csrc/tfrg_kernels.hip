@@ -355,6 +355,20 @@ __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2
   }
 }
 
+// put_inline at column position base + r, base wave-uniform when the slot is (the template path:
+// scalar column base + 32-bit record offset stores); bounds as put_inline
+__device__ __forceinline__ void put_inline_at(const DevOut& o, uint32_t kind, uint2 lc, uint64_t base, uint32_t r) {
+  const uint64_t dst = base + r;
+  if (kind == TFRG_KIND_INT64) {
+    if (dst < o.cap_i64) (o.i64 + base)[r] = (int64_t)(((uint64_t)lc.y << 32) | lc.x);
+  } else if (kind == TFRG_KIND_FLOAT) {
+    if (dst < o.cap_f32) (o.f32 + base)[r] = lc.x;
+  } else if (dst < o.cap_b) {
+    (o.b_off + base)[r] = lc.x;
+    (o.b_len + base)[r] = lc.y;
+  }
+}
+
 template <bool L>
 struct CountSinkT {
   using ord_t = std::conditional_t<L, lds_u16, uint16_t>;
@@ -473,7 +487,7 @@ struct CountSinkT {
                    // copies the value back into it if the slot's placement fails)
         const uint32_t sw = spec[slot];
         if (sw && (cw & kCountInline)) {
-          put_inline(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u) + r);
+          put_inline_at(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u), r);
           return;
         }
       }
@@ -1364,6 +1378,53 @@ __device__ __forceinline__ int tpl_match(const FastSrc& fs, const uint32_t* tpl,
   return hit;
 }
 
+// tpl_match, and for the template that matches, the raw CRC of the record's variable bits from its
+// first variable byte on (tfrg_internal.h kTplCrcK): tcrc = U(0, (M & ~mask)[v0, L)), computed from the
+// words the match reads anyway (crc = false: the match alone).
+template <int R>
+__device__ __forceinline__ int tpl_match_crc(const FastSrc& fs, const uint32_t* tpl, uint32_t n_tpl,
+                                             const LdsTab<R>& T, bool crc, uint32_t& tcrc) {
+  int hit = -1;
+  tcrc = 0;
+  for (uint32_t t = 0; t < n_tpl; ++t) {
+    const uint32_t* Tp = tpl + t * kTplWords;
+    if (hit < 0 && fs.L == Tp[0]) {
+      const uint32_t nw = Tp[2];
+      const uint32_t v0 = Tp[kTplV0];
+      const uint32_t w0 = crc && v0 != 0xffffffffu ? v0 >> 2 : nw;
+      uint32_t diff = 0, c = 0;
+      // payload words from the aligned stage words: one LDS read per word (the previous one carried)
+      const uint32_t* SW = reinterpret_cast<const uint32_t*>(fs.l) + (fs.p >> 2);
+      const uint32_t sh = fs.p & 3u;
+      uint32_t prev = SW[0];
+      for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t next = SW[w + 1u];
+        const uint32_t x = __builtin_amdgcn_alignbyte(next, prev, sh), m = Tp[kTplMask + w];
+        prev = next;
+        diff |= (x ^ Tp[kTplBytes + w]) & m;
+        if (w >= w0) {
+          const uint32_t rem = fs.L - 4u * w;
+          if (rem >= 4u) {
+            c = T.step4(c ^ (x & ~m));
+          } else {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
+            const uint32_t y = c ^ (x & ~m & bytes_mask(rem));
+            uint32_t u = T(rem - 1u, y & 0xffu);
+            const uint32_t u1 = T(rem >= 2u ? rem - 2u : 0u, (y >> 8) & 0xffu), u2 = T(0u, (y >> 16) & 0xffu);
+            u ^= rem >= 2u ? u1 : 0u;
+            u ^= rem == 3u ? u2 : 0u;
+            c = u ^ (c >> (8u * rem));
+          }
+        }
+      }
+      if (!diff) {
+        hit = (int)t;
+        tcrc = c;
+      }
+    }
+  }
+  return hit;
+}
+
 // The matched template's dict, exactly as fast_walk builds it for this record: slots, ranks and
 // count words from the template, list locations or the inline values read from the record.
 template <class Sink>
@@ -1388,7 +1449,8 @@ __device__ __forceinline__ void tpl_put(const FastSrc& fs, const uint32_t* T, Si
 // payload_crc = false leaves the payload CRC of a record above lane_max to k_wave_count.
 template <int R, bool STAGED>
 __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, const LdsTab<R>& T, const uint8_t* stage,
-                                               uint64_t lo16, bool payload_crc = true) {
+                                               uint64_t lo16, bool payload_crc = true, const uint32_t* tp = nullptr,
+                                               uint32_t tcrc = 0) {
   if (B.flags & kFlagPayloadOnly) return;
   const bool do_crc = !(B.flags & kFlagNoCrc);
   const uint64_t D = v.e - v.st;
@@ -1405,21 +1467,23 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   }
   if (lenf == v.en - v.st - 16) v.verdict |= TFRG_V_LEN_MATCH;
   if (do_crc && D >= 12) {
-    uint32_t c, stored;
+    uint32_t want, stored;
     if constexpr (STAGED) {
-      // the 8 length bytes are the two words just read: two slicing steps, any alignment
-      c = ~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1);
       stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
+      // a template's length: the masked CRC of its 8 length bytes is a constant of the template;
+      // else the two words just read, two slicing steps at any alignment
+      want = tp && lenf == (uint64_t)tp[0] ? tp[kTplLenCrc] : crc_mask(~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1));
     } else {
-      c = crc_serial<R>(B.bytes, v.st, v.st + 8, T);
+      want = crc_mask(crc_serial<R>(B.bytes, v.st, v.st + 8, T));
       stored = load_u32_unaligned(B.bytes, v.st + 8);
     }
-    if (crc_mask(c) == stored) v.verdict |= TFRG_V_LEN_CRC;
+    if (want == stored) v.verdict |= TFRG_V_LEN_CRC;
   }
   if (do_crc && payload_crc && D >= 16) {
     uint32_t c, stored;
     if constexpr (STAGED) {
-      c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+      c = tp && tp[kTplV0] != 0xffffffffu ? ~(tcrc ^ tp[kTplCrcK])
+                                          : crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
       stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
     } else {
       c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
@@ -1597,13 +1661,16 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     bool done = false;
     bool tried = false;
     if (staged && span_rec) {
-      frame_verdicts<R, true>(B, v, T, stage, lo16);
+      // a known record shape (template) first: it also carries most of the record's CRC-32C work
+      const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
+      uint32_t tcrc = 0;
+      const bool fcrc = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
+      const int tm = sc.n_tpl ? tpl_match_crc<R>(fs, tpl_l, sc.n_tpl, T, fcrc, tcrc) : -1;
+      frame_verdicts<R, true>(B, v, T, stage, lo16, true, tm >= 0 ? tpl_l + (uint32_t)tm * kTplWords : nullptr, tcrc);
       PHASE_MARK(p2);
       PHASE_ADD(17, p1, p2);
       sink.fast_reset(S);
       if (strict_pass(B, v.verdict, true)) {  // (strict mode: a CRC failure is the slow kernel's)
-        const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-        const int tm = sc.n_tpl ? tpl_match(fs, tpl_l, sc.n_tpl) : -1;
         if (tm >= 0) {  // a known record shape: its dict without the walk
           tpl_put(fs, tpl_l + (uint32_t)tm * kTplWords, sink);
           done = true;
@@ -1672,10 +1739,11 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     for (uint32_t k = 0; k < S; ++k) {
       const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
       const uint32_t c = ov ? sink.count_of(k) : 0u;
-      if (done) {
-        const size_t at = (size_t)k * B.n + r;
-        o.order[at] = (uint16_t)ov;
-        o.count[at] = c;
+      if (done) {  // (slot column bases are wave-uniform: scalar base + 32-bit record offset stores)
+        uint16_t* const ord_k = o.order + (size_t)rfl32(k) * B.n;
+        uint32_t* const cnt_k = o.count + (size_t)rfl32(k) * B.n;
+        ord_k[r] = (uint16_t)ov;
+        cnt_k[r] = c;
       }
       const uint32_t x = c & ~kCountInline;
       const uint64_t nz = __ballot(x != 0u);
@@ -1684,7 +1752,8 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
       }
       if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
-        if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
+        uint32_t* const rs_k = o.rs + (size_t)rfl32(k) * (B.n + 1);
+        if (valid) rs_k[r] = r;
         const uint64_t irm = __ballot(valid && !stg && !(done && c == (1u | kCountInline)));
         if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
       }
