@@ -355,20 +355,6 @@ __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2
   }
 }
 
-// put_inline at column position base + r, base wave-uniform when the slot is (the template path:
-// scalar column base + 32-bit record offset stores); bounds as put_inline
-__device__ __forceinline__ void put_inline_at(const DevOut& o, uint32_t kind, uint2 lc, uint64_t base, uint32_t r) {
-  const uint64_t dst = base + r;
-  if (kind == TFRG_KIND_INT64) {
-    if (dst < o.cap_i64) (o.i64 + base)[r] = (int64_t)(((uint64_t)lc.y << 32) | lc.x);
-  } else if (kind == TFRG_KIND_FLOAT) {
-    if (dst < o.cap_f32) (o.f32 + base)[r] = lc.x;
-  } else if (dst < o.cap_b) {
-    (o.b_off + base)[r] = lc.x;
-    (o.b_len + base)[r] = lc.y;
-  }
-}
-
 template <bool L>
 struct CountSinkT {
   using ord_t = std::conditional_t<L, lds_u16, uint16_t>;
@@ -487,7 +473,7 @@ struct CountSinkT {
                    // copies the value back into it if the slot's placement fails)
         const uint32_t sw = spec[slot];
         if (sw && (cw & kCountInline)) {
-          put_inline_at(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u), r);
+          put_inline(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u) + r);
           return;
         }
       }
@@ -1739,11 +1725,10 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     for (uint32_t k = 0; k < S; ++k) {
       const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
       const uint32_t c = ov ? sink.count_of(k) : 0u;
-      if (done) {  // (slot column bases are wave-uniform: scalar base + 32-bit record offset stores)
-        uint16_t* const ord_k = o.order + (size_t)rfl32(k) * B.n;
-        uint32_t* const cnt_k = o.count + (size_t)rfl32(k) * B.n;
-        ord_k[r] = (uint16_t)ov;
-        cnt_k[r] = c;
+      if (done) {
+        const size_t at = (size_t)k * B.n + r;
+        o.order[at] = (uint16_t)ov;
+        o.count[at] = c;
       }
       const uint32_t x = c & ~kCountInline;
       const uint64_t nz = __ballot(x != 0u);
@@ -1752,8 +1737,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
       }
       if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
-        uint32_t* const rs_k = o.rs + (size_t)rfl32(k) * (B.n + 1);
-        if (valid) rs_k[r] = r;
+        if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
         const uint64_t irm = __ballot(valid && !stg && !(done && c == (1u | kCountInline)));
         if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
       }
