@@ -66,6 +66,17 @@ void tfrg_free(void* p);
  * [starts[i], ends[i]) of src back to back into dst (NULL: only sizes them); returns the total. */
 uint64_t tfrg_gather_ranges(const uint8_t* src, const uint64_t* starts, const uint64_t* ends, int64_t n,
                             uint8_t* dst);
+/* Key discovery before a device decode (no reference counterpart: the keys and kinds that
+ * decoder.pyx:130-199 would meet). Parses the Example -> Features -> map entries of the n records
+ * [start[i], end[i]) of bytes (framed, or bare payloads with TFRG_FLAG_PAYLOAD_ONLY) and writes up
+ * to cap distinct (key offset, key length, kind) u64 triples: absolute key offsets into bytes, kind =
+ * the field number of the entry's Feature (1 bytes_list, 2 float_list, 3 int64_list). Only canonical
+ * records seed (Example = features fields, each map entry = key then value, each Feature = one list
+ * field); any other record is left to the device decode's schema-miss pass, which follows the
+ * reference's semantics. Returns the triple count. Seeding the key table with them spares a first
+ * decode the exact walker's schema-miss pass. */
+int64_t tfrg_scan_keys(const uint8_t* bytes, uint64_t nbytes, const uint64_t* start, const uint64_t* end, int64_t n,
+                       uint32_t flags, uint64_t* out_triples, int64_t cap);
 
 /* Compressed TFRecord files (TensorFlow TFRecordOptions "ZLIB" / "GZIP": the whole framed stream
  * deflated; claimed by the reference's README.md:14, not implemented there). tfrg_compression_of

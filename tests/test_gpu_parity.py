@@ -133,8 +133,14 @@ def test_c1_shape_vs_oracle(dec, orc):
     assert (r.verdict == 7).all()
     bad = _compare_to_oracle(r, orc, buf, st, en)  # every record: values, key order, CRC verdicts
     assert not bad, bad[:10]
-    labels = r.i64[int(r.slot_base[r.slot_key.index("label")]) :][:65536]
+    labels = r.i64[int(r.slot_base[_slot(r, "label", 3)]) :][:65536]
     assert np.array_equal(labels, np.arange(65536) % 1000)
+
+
+def _slot(r, key, kind):
+    """The slot of (key, kind): the decoder's key table outlives batches, so a key may hold slots of
+    several kinds."""
+    return next(s for s, k in enumerate(r.slot_key) if k == key and r.slot_kind[s] == kind)
 
 
 def test_row_splits_across_spine_chunks(dec):
@@ -155,14 +161,15 @@ def test_row_splits_across_spine_chunks(dec):
     has = np.ones(131072, bool)
     has[65536::7] = False
     has = np.tile(has, 20)
-    lab = r.slot_key.index("label")
+    lab = _slot(r, "label", 3)
     want_rs = np.concatenate([[0], np.cumsum(has)])
     assert np.array_equal(r.row_splits[lab], want_rs)
     want = np.tile(np.concatenate([np.arange(65536) % 1000, (np.arange(65536) % 1000)[np.arange(65536) % 7 != 0]]), 20)
     got = r.i64[int(r.slot_base[lab]) : int(r.slot_base[lab]) + want.size]
     assert np.array_equal(got, want)
-    ids = r.slot_key.index("id")
-    assert np.array_equal(r.row_splits[ids], np.arange(n + 1))
+    ids = _slot(r, "id", 1)
+    bad = np.flatnonzero(r.row_splits[ids] != np.arange(n + 1))
+    assert bad.size == 0, (bad.size, bad[:8].tolist(), len(r.slot_key), ids)
 
 
 def test_lane_crc_verdicts_every_alignment(dec, orc):

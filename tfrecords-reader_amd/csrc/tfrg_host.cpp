@@ -11,6 +11,8 @@
 #include <unistd.h>
 
 #include <string>
+#include <unordered_set>
+#include <vector>
 
 #include <zlib.h>
 
@@ -312,6 +314,147 @@ uint64_t tfrg_gather_ranges(const uint8_t* src, const uint64_t* starts, const ui
     at += len;
   }
   return at;
+}
+
+}  // extern "C"
+
+// ---- key discovery (tfrg_scan_keys) -----------------------------------------------------------
+namespace {
+struct PbCur {  // bounded protobuf cursor over [p, e)
+  const uint8_t* p;
+  const uint8_t* e;
+  bool varint(uint64_t& v) {
+    v = 0;
+    for (int s = 0; s < 64 && p < e; s += 7) {
+      const uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return true;
+    }
+    return false;
+  }
+  // next field: number, wire type, and for wire type 2 its body [bp, bp + bl)
+  bool field(uint64_t& fn, uint32_t& wt, const uint8_t*& bp, uint64_t& bl) {
+    uint64_t tag;
+    if (p >= e || !varint(tag)) return false;
+    fn = tag >> 3;
+    wt = (uint32_t)(tag & 7);
+    uint64_t v;
+    switch (wt) {
+      case 0: return varint(v);
+      case 1: if (e - p < 8) return false; p += 8; return true;
+      case 5: if (e - p < 4) return false; p += 4; return true;
+      case 2:
+        if (!varint(bl) || bl > (uint64_t)(e - p)) return false;
+        bp = p;
+        p += bl;
+        return true;
+      default: return false;
+    }
+  }
+};
+
+// a list message of a well-formed value list (bytes: length-delimited elements; float: packed
+// 4-byte multiples or fixed32; int64: packed or single varints of <= 10 bytes)
+bool list_ok(uint64_t kind, const uint8_t* p, uint64_t n) {
+  PbCur c{p, p + n};
+  uint64_t fn, bl;
+  uint32_t wt;
+  const uint8_t* bp = nullptr;
+  while (c.p < c.e) {
+    const uint8_t* at = c.p;
+    if (!c.field(fn, wt, bp, bl) || fn != 1) return false;
+    if (kind == 1) {
+      if (wt != 2) return false;
+    } else if (kind == 2) {
+      if (!(wt == 5 || (wt == 2 && bl % 4 == 0))) return false;
+    } else {
+      if (wt == 0) {
+        if (c.p - at > 11) return false;  // tag + a varint of <= 10 bytes
+      } else if (wt == 2) {
+        PbCur v{bp, bp + bl};
+        while (v.p < v.e) {
+          const uint8_t* s0 = v.p;
+          uint64_t x;
+          if (!v.varint(x) || v.p - s0 > 10) return false;
+        }
+      } else {
+        return false;
+      }
+    }
+  }
+  return true;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t tfrg_scan_keys(const uint8_t* bytes, uint64_t nbytes, const uint64_t* start, const uint64_t* end, int64_t n,
+                       uint32_t flags, uint64_t* out, int64_t cap) {
+  const bool framed = !(flags & 1u);  // TFRG_FLAG_PAYLOAD_ONLY
+  std::unordered_set<std::string> seen;
+  std::vector<std::pair<std::string, uint64_t>> rec;  // this record's (key + kind, key offset)
+  int64_t k = 0;
+  for (int64_t i = 0; i < n && k < cap; ++i) {
+    uint64_t a = start[i], b = end[i];
+    if (b > nbytes || a > b) continue;
+    if (framed) {
+      if (b - a < 16) continue;
+      a += 12;
+      b -= 4;
+    }
+    // only a canonical record seeds keys (Example = features fields, Features = map entries of key
+    // then value, a Feature = one list field): its keys and kinds are exactly what the reference
+    // decoder meets; any other record is left to the device's schema-miss pass
+    rec.clear();
+    bool ok = true;
+    PbCur ex{bytes + a, bytes + b};
+    uint64_t fn, bl;
+    uint32_t wt;
+    const uint8_t* bp = nullptr;
+    while (ok && ex.p < ex.e) {
+      if (!ex.field(fn, wt, bp, bl) || fn != 1 || wt != 2) {
+        ok = false;
+        break;
+      }
+      PbCur fs{bp, bp + bl};
+      const uint8_t* ep = nullptr;
+      uint64_t el;
+      while (ok && fs.p < fs.e) {
+        if (!fs.field(fn, wt, ep, el) || fn != 1 || wt != 2) {
+          ok = false;
+          break;
+        }
+        PbCur en{ep, ep + el};
+        const uint8_t *kp = nullptr, *vp = nullptr;
+        uint64_t kl = 0, vl = 0, f2 = 0, ql = 0;
+        uint32_t w2 = 0;
+        const uint8_t* q = nullptr;
+        if (!en.field(f2, w2, kp, kl) || f2 != 1 || w2 != 2 || !en.field(f2, w2, vp, vl) || f2 != 2 || w2 != 2 ||
+            en.p != en.e) {
+          ok = false;
+          break;
+        }
+        PbCur fe{vp, vp + vl};
+        if (!fe.field(f2, w2, q, ql) || f2 < 1 || f2 > 3 || w2 != 2 || fe.p != fe.e || !list_ok(f2, q, ql)) {
+          ok = false;
+          break;
+        }
+        std::string id((const char*)kp, kl);
+        id.push_back((char)f2);
+        rec.emplace_back(std::move(id), (uint64_t)(kp - bytes));
+      }
+    }
+    if (!ok) continue;
+    for (auto& [id, off] : rec) {
+      if (k >= cap) break;
+      if (!seen.insert(id).second) continue;
+      out[3 * k] = off;
+      out[3 * k + 1] = id.size() - 1;
+      out[3 * k + 2] = (uint8_t)id.back();
+      ++k;
+    }
+  }
+  return k;
 }
 
 int tfrg_idx_save(const char* idx_path, const uint64_t* triples, int64_t n) {

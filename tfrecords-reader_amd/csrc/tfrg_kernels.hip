@@ -342,6 +342,8 @@ __device__ int walk_example(S& s, Sink& sink, int64_t& aux) {
 // never a flat one); !L: in the global order / count columns (key tables too large for LDS).
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+// constant address space: loads at wave-uniform indices compile to scalar loads (s_load, SGPRs)
+typedef __attribute__((address_space(4))) const uint32_t cu32;
 
 // single value stored in the loc word by the count pass
 __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2 lc, uint64_t dst) {
@@ -352,6 +354,66 @@ __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2
   } else if (dst < o.cap_b) {
     o.b_off[dst] = lc.x;
     o.b_len[dst] = lc.y;
+  }
+}
+
+// DevSchema::spec word of a wave-uniform slot, in an SGPR (TFRG_TPL_SMEM: HBM, else the LDS copy)
+__device__ __forceinline__ uint32_t spec_word_u(const uint32_t* spec, uint32_t slot) {
+#if TFRG_TPL_SMEM
+  return ((cu32*)spec)[slot];
+#else
+  return __builtin_amdgcn_readfirstlane(spec[slot]);
+#endif
+}
+
+// Speculative placement target of one slot (DevSchema::spec), staged in LDS by the lane kernel's
+// prologue: the value column addresses at n * rank and the records r < lim that fit its capacity.
+// The stores then need no DevOut field (seven pointers and capacities, which the register allocator
+// otherwise kept spilled in VGPR lanes and reloaded with v_readlane per stored value).
+// Layout: 8 u32 words per slot: [0, 2) p1 = int64 / float column, or bytes_list offsets, [2, 4) p2 =
+// bytes_list lengths, [4] lim (records r < lim are stored: capacity), [5] kind.
+typedef uint32_t spec_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) spec_u32x4 lds_spec_t;
+constexpr uint32_t kSpecTgtWords = 8;
+
+__device__ __forceinline__ void spec_target(uint32_t* dst, const DevOut& o, uint32_t sw, uint32_t n) {
+  const uint32_t kind = sw & 3u;
+  uint64_t p1 = 0, p2 = 0;
+  uint32_t lim = 0;
+  if (sw) {
+    const uint64_t base = (uint64_t)n * ((sw >> 2) - 1u);
+    const uint64_t cap = kind == TFRG_KIND_INT64 ? o.cap_i64 : kind == TFRG_KIND_FLOAT ? o.cap_f32 : o.cap_b;
+    lim = cap > base ? (cap - base < n ? (uint32_t)(cap - base) : n) : 0u;
+    if (kind == TFRG_KIND_INT64) {
+      p1 = (uint64_t)(o.i64 + base);
+    } else if (kind == TFRG_KIND_FLOAT) {
+      p1 = (uint64_t)(o.f32 + base);
+    } else {
+      p1 = (uint64_t)(o.b_off + base);
+      p2 = (uint64_t)(o.b_len + base);
+    }
+  }
+  dst[0] = (uint32_t)p1;
+  dst[1] = (uint32_t)(p1 >> 32);
+  dst[2] = (uint32_t)p2;
+  dst[3] = (uint32_t)(p2 >> 32);
+  dst[4] = lim;
+  dst[5] = kind;
+  dst[6] = dst[7] = 0;
+}
+
+// put_inline at a staged target (record r of the batch)
+__device__ __forceinline__ void put_spec(const lds_spec_t* t, uint2 lc, uint32_t r) {
+  const spec_u32x4 a = t[0], b = t[1];
+  if (r >= b.x) return;
+  const uint64_t p1 = ((uint64_t)a.y << 32) | a.x;
+  if (b.y == TFRG_KIND_INT64) {
+    reinterpret_cast<uint2*>(p1)[r] = lc;
+  } else if (b.y == TFRG_KIND_FLOAT) {
+    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
+  } else {
+    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
+    reinterpret_cast<uint32_t*>(((uint64_t)a.w << 32) | a.z)[r] = lc.y;
   }
 }
 
@@ -371,6 +433,8 @@ struct CountSinkT {
   bool leader;       // issues global writes and atomics
   cnt_t* cnt = nullptr;  // LDS value counts, same layout as ord (L only)
   const lds_u32* spec = nullptr;  // DevSchema::spec staged in LDS (L only; null = off)
+  const lds_spec_t* spec_t = nullptr;  // its targets (kSpecTgtWords per slot)
+  const uint32_t* spec_u = nullptr;       // DevSchema::spec for uniform slots (scalar reads, as TplRef)
 
   __device__ __forceinline__ void reset() {
     for (uint32_t k = 0; k < sc->n_slots; ++k) ord[(size_t)k * ostride] = 0;
@@ -473,12 +537,28 @@ struct CountSinkT {
                    // copies the value back into it if the slot's placement fails)
         const uint32_t sw = spec[slot];
         if (sw && (cw & kCountInline)) {
-          put_inline(*o, sw & 3u, lv, (uint64_t)n * ((sw >> 2) - 1u) + r);
+          put_spec(spec_t + 2u * slot, lv, r);
           return;
         }
       }
     }
     o->loc[at] = lv;
+  }
+
+  // fast_put at a wave-uniform slot / rank / count word (template entries): the speculative
+  // placement test is a scalar branch
+  __device__ __forceinline__ void fast_put_u(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
+    if constexpr (L) {
+      ord[(size_t)slot * ostride] = (uint16_t)rk;
+      cnt[(size_t)slot * ostride] = cw;
+      if (spec_u && (cw & kCountInline) && spec_word_u(spec_u, slot)) {
+        put_spec(spec_t + 2u * slot, lv, r);
+        return;
+      }
+      o->loc[(size_t)slot * n + r] = lv;
+    } else {
+      fast_put(slot, rk, cw, lv);
+    }
   }
 
   // final count of a present slot (LDS, or read back from this thread's own column write)
@@ -534,6 +614,9 @@ struct MaskSink {
     o->loc[at] = lv;
     pm |= 1ull << slot;
     __atomic_fetch_add(&tsl[slot], cw & ~kCountInline, __ATOMIC_RELAXED);
+  }
+  __device__ __forceinline__ void fast_put_u(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
+    fast_put(slot, rk, cw, lv);
   }
   __device__ __forceinline__ void rollback() {  // this thread's own column writes, read back
     for (uint64_t m = pm; m; m &= m - 1) {
@@ -1348,85 +1431,131 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
   return ok ? TFRG_OK : kBail;
 }
 
-// Record-shape templates (tfrg_internal.h, learned on the host): the first template this payload
-// equals under its mask, or -1 (wave-uniform loop over the templates, ~5 VALU per payload word).
-__device__ __forceinline__ int tpl_match(const FastSrc& fs, const uint32_t* tpl, uint32_t n_tpl) {
-  int hit = -1;
-  for (uint32_t t = 0; t < n_tpl; ++t) {
-    const uint32_t* T = tpl + t * kTplWords;
-    if (hit < 0 && fs.L == T[0]) {
-      const uint32_t nw = T[2];
-      uint32_t diff = 0;
-      for (uint32_t w = 0; w < nw; ++w) diff |= (fs.u32(4u * w) ^ T[kTplBytes + w]) & T[kTplMask + w];
-      if (!diff) hit = (int)t;
-    }
-  }
-  return hit;
-}
+// Record-shape templates (tfrg_internal.h, learned on the host) are read through the constant
+// address space: every template word is indexed by wave-uniform values (template, word, entry), so
+// the loads are scalar (s_load into SGPRs, the VALU operands directly) and the loop bounds, the
+// CRC start word and the entry modes are scalar branches, not exec-mask regions.
+#ifndef TFRG_TPL_SMEM
+#define TFRG_TPL_SMEM 0
+#endif
+// One template's words. Control words (lengths, entry fields, CRC constants) are wave-uniform:
+// u() returns them in SGPRs, so the loops and mode tests over them are scalar branches; d() reads
+// the per-word bytes / mask as VALU operands. TFRG_TPL_SMEM = 1 reads them with scalar loads from
+// HBM, 0 from the copy staged in LDS (a broadcast read, then v_readfirstlane for u()).
+struct TplRef {
+#if TFRG_TPL_SMEM
+  cu32* p;
+  __device__ __forceinline__ uint32_t u(uint32_t i) const { return p[i]; }
+  __device__ __forceinline__ uint32_t d(uint32_t i) const { return p[i]; }
+#else
+  const uint32_t* p;
+  __device__ __forceinline__ uint32_t u(uint32_t i) const { return __builtin_amdgcn_readfirstlane(p[i]); }
+  __device__ __forceinline__ uint32_t d(uint32_t i) const { return p[i]; }
+#endif
+  __device__ __forceinline__ TplRef at(uint32_t t) const { return TplRef{p + t * kTplWords}; }
+};
 
-// tpl_match, and for the template that matches, the raw CRC of the record's variable bits from its
-// first variable byte on (tfrg_internal.h kTplCrcK): tcrc = U(0, (M & ~mask)[v0, L)), computed from the
-// words the match reads anyway (crc = false: the match alone).
+// match result of one lane
+struct TplHit {
+  int t = -1;          // the first template the payload equals under its mask, -1 none
+  bool pc = false;     // pcrc holds the payload CRC-32C (the template defines v0)
+  uint32_t pcrc = 0;   // CRC-32C of the payload: ~(K ^ U(0, (M & ~mask)[v0, L)))
+  uint32_t lcrc = 0;   // masked CRC-32C of the 8 length bytes of L (a template constant)
+};
+
+// Templates in order, each over the lanes whose payload length is its L and that matched none
+// before it (a wave-uniform loop; a template no lane can match costs one ballot). The words the
+// match reads also feed the CRC of the variable bits from the template's first variable byte on
+// (crc = false: the match alone). The payload words come from the aligned stage words, one LDS
+// read per word (the previous one carried, one alignbyte).
 template <int R>
-__device__ __forceinline__ int tpl_match_crc(const FastSrc& fs, const uint32_t* tpl, uint32_t n_tpl,
-                                             const LdsTab<R>& T, bool crc, uint32_t& tcrc) {
-  int hit = -1;
-  tcrc = 0;
+__device__ __forceinline__ TplHit tpl_match_u(const FastSrc& fs, bool cand0, TplRef tg, uint32_t n_tpl,
+                                              const LdsTab<R>& T, bool crc) {
+  TplHit h;
+  const uint32_t* SW = reinterpret_cast<const uint32_t*>(fs.l) + (fs.p >> 2);
+  const uint32_t sh = fs.p & 3u;
   for (uint32_t t = 0; t < n_tpl; ++t) {
-    const uint32_t* Tp = tpl + t * kTplWords;
-    if (hit < 0 && fs.L == Tp[0]) {
-      const uint32_t nw = Tp[2];
-      const uint32_t v0 = Tp[kTplV0];
-      const uint32_t w0 = crc && v0 != 0xffffffffu ? v0 >> 2 : nw;
-      uint32_t diff = 0, c = 0;
-      // payload words from the aligned stage words: one LDS read per word (the previous one carried)
-      const uint32_t* SW = reinterpret_cast<const uint32_t*>(fs.l) + (fs.p >> 2);
-      const uint32_t sh = fs.p & 3u;
-      uint32_t prev = SW[0];
-      for (uint32_t w = 0; w < nw; ++w) {
-        const uint32_t next = SW[w + 1u];
-        const uint32_t x = __builtin_amdgcn_alignbyte(next, prev, sh), m = Tp[kTplMask + w];
-        prev = next;
-        diff |= (x ^ Tp[kTplBytes + w]) & m;
-        if (w >= w0) {
-          const uint32_t rem = fs.L - 4u * w;
-          if (rem >= 4u) {
-            c = T.step4(c ^ (x & ~m));
-          } else {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
-            const uint32_t y = c ^ (x & ~m & bytes_mask(rem));
-            uint32_t u = T(rem - 1u, y & 0xffu);
-            const uint32_t u1 = T(rem >= 2u ? rem - 2u : 0u, (y >> 8) & 0xffu), u2 = T(0u, (y >> 16) & 0xffu);
-            u ^= rem >= 2u ? u1 : 0u;
-            u ^= rem == 3u ? u2 : 0u;
-            c = u ^ (c >> (8u * rem));
+    const TplRef Tp = tg.at(t);
+    const uint32_t L = Tp.u(0);
+    // (an opaque copy of L: inside the branch below the compiler would otherwise substitute the
+    // lane's own length for it and keep the CRC's byte counts in VGPRs)
+    uint32_t Lu = L;
+    asm("" : "+s"(Lu));
+    const bool cand = cand0 && h.t < 0 && fs.L == L;
+    if (__ballot(cand) == 0) continue;
+    if (cand) {
+      const uint32_t nw = Tp.u(2), v0 = Tp.u(kTplV0);
+      const bool pc = crc && v0 != 0xffffffffu;
+      const uint32_t w0 = pc ? v0 >> 2 : nw;
+      uint32_t diff = 0, c = 0, prev = SW[0];
+      // four words per step: template words beyond L are zero (mask 0), the stage has 64 bytes of
+      // slack past any record
+      for (uint32_t w = 0; w < nw; w += 4u) {
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t next = SW[w + 1u + i];
+          x[i] = __builtin_amdgcn_alignbyte(next, prev, sh);
+          prev = next;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) diff |= (x[i] ^ Tp.d(kTplBytes + w + i)) & Tp.d(kTplMask + w + i);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t wi = w + i;
+          if (wi >= w0 && wi < nw) {  // (scalar branch)
+            const uint32_t m = Tp.d(kTplMask + wi), rem = Lu - 4u * wi;
+            if (rem >= 4u) {
+              c = T.step4(c ^ (x[i] & ~m));
+            } else {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
+              const uint32_t y = c ^ (x[i] & ~m & bytes_mask(rem));
+              uint32_t u = T(rem - 1u, y & 0xffu);
+              if (rem >= 2u) u ^= T(rem - 2u, (y >> 8) & 0xffu);
+              if (rem == 3u) u ^= T(0u, (y >> 16) & 0xffu);
+              c = u ^ (c >> (8u * rem));
+            }
           }
         }
       }
       if (!diff) {
-        hit = (int)t;
-        tcrc = c;
+        h.t = (int)t;
+        h.pc = pc;
+        h.pcrc = ~(c ^ Tp.u(kTplCrcK));
+        h.lcrc = Tp.u(kTplLenCrc);
       }
     }
   }
-  return hit;
+  return h;
 }
 
 // The matched template's dict, exactly as fast_walk builds it for this record: slots, ranks and
-// count words from the template, list locations or the inline values read from the record.
+// count words from the template (scalar), list locations or the inline values read from the record.
 template <class Sink>
-__device__ __forceinline__ void tpl_put(const FastSrc& fs, const uint32_t* T, Sink& sink) {
-  const uint32_t ne = T[1];
+__device__ __forceinline__ void tpl_put_u(const FastSrc& fs, TplRef Tp, Sink& sink) {
+  const uint32_t ne = Tp.u(1);
   for (uint32_t e = 0; e < ne; ++e) {
-    const uint4 d = *reinterpret_cast<const uint4*>(T + kTplEnt + 4u * e);
-    const uint32_t mode = d.x >> 24, a = d.w & 0xffffu, b = d.w >> 16;
+    const uint32_t dx = Tp.u(kTplEnt + 4u * e), dy = Tp.u(kTplEnt + 4u * e + 1u), dz = Tp.u(kTplEnt + 4u * e + 2u),
+                   dw = Tp.u(kTplEnt + 4u * e + 3u);
+    const uint32_t mode = dx >> 24, a = dw & 0xffffu, b = dw >> 16;
     uint2 lv;
     if (mode == 0u) lv = make_uint2(a, b);                                       // (list offset, length)
     else if (mode == 1u) lv = make_uint2(vgroups(fs.u32(a), bytes_mask(b)), 0u);  // one int64 varint
     else if (mode == 2u) lv = make_uint2(fs.u32(a), 0u);                          // one float
     else lv = make_uint2((uint32_t)(fs.base + a), b);                             // one bytes element
-    sink.fast_put(d.x & 0xffffffu, d.y, d.z, lv);
+    sink.fast_put_u(dx & 0xffffffu, dy, dz, lv);
   }
   sink.rank = ne;
+}
+
+// tpl_put_u for every lane with put set, template by template (wave-uniform loop)
+template <class Sink>
+__device__ __forceinline__ void tpl_put_all(const FastSrc& fs, bool put, int t_hit, TplRef tg, uint32_t n_tpl,
+                                            Sink& sink) {
+  for (uint32_t t = 0; t < n_tpl; ++t) {
+    const bool mine = put && t_hit == (int)t;
+    if (__ballot(mine) == 0) continue;
+    if (mine) tpl_put_u(fs, tg.at(t), sink);
+  }
 }
 
 // Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
@@ -1435,8 +1564,7 @@ __device__ __forceinline__ void tpl_put(const FastSrc& fs, const uint32_t* T, Si
 // payload_crc = false leaves the payload CRC of a record above lane_max to k_wave_count.
 template <int R, bool STAGED>
 __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, const LdsTab<R>& T, const uint8_t* stage,
-                                               uint64_t lo16, bool payload_crc = true, const uint32_t* tp = nullptr,
-                                               uint32_t tcrc = 0) {
+                                               uint64_t lo16, bool payload_crc = true, const TplHit* th = nullptr) {
   if (B.flags & kFlagPayloadOnly) return;
   const bool do_crc = !(B.flags & kFlagNoCrc);
   const uint64_t D = v.e - v.st;
@@ -1458,7 +1586,8 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
       stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
       // a template's length: the masked CRC of its 8 length bytes is a constant of the template;
       // else the two words just read, two slicing steps at any alignment
-      want = tp && lenf == (uint64_t)tp[0] ? tp[kTplLenCrc] : crc_mask(~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1));
+      want = th && th->t >= 0 && lenf == (uint64_t)v.L ? th->lcrc
+                                                        : crc_mask(~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1));
     } else {
       want = crc_mask(crc_serial<R>(B.bytes, v.st, v.st + 8, T));
       stored = load_u32_unaligned(B.bytes, v.st + 8);
@@ -1468,8 +1597,8 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   if (do_crc && payload_crc && D >= 16) {
     uint32_t c, stored;
     if constexpr (STAGED) {
-      c = tp && tp[kTplV0] != 0xffffffffu ? ~(tcrc ^ tp[kTplCrcK])
-                                          : crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+      c = th && th->t >= 0 && th->pc ? th->pcrc
+                                     : crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
       stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
     } else {
       c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
@@ -1534,6 +1663,54 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)rfl32((uint32_t)(x >> 32)) << 32) | rfl32((uint32_t)x);
 }
 
+#ifndef TFRG_LANE_PREF
+#define TFRG_LANE_PREF 0
+#endif
+// The lane kernel's staging decision for one wave's records, from their offsets alone: the span of
+// the records the lane walk takes (fast path, <= lane_max), staged when it fits kStageBytes.
+__device__ __forceinline__ bool lane_span(const DevBatch& B, uint64_t st, uint64_t en, bool valid, bool fast_ok,
+                                          uint32_t lane_max, uint64_t& lo16, uint64_t& hi) {
+  bool sr = false;
+  uint64_t a = 0, b = 0;
+  if (valid) {
+    const RecView v = rec_view_se(B, st, en);
+    sr = fast_ok && v.status == TFRG_OK && v.e - v.st <= lane_max;
+    a = v.st;
+    b = v.e;
+  }
+  uint64_t lo;
+  wave_span(sr, a, b, lo, hi);
+  lo = rfl64(lo);
+  hi = rfl64(hi);
+  lo16 = lo & ~15ull;
+  return hi > lo && hi - lo16 <= kStageBytes;
+}
+
+// One wave's lane-kernel span (<= 4 KiB) held in registers between its loads and its LDS stores:
+// the next iteration's bytes are requested before this iteration's records are decoded.
+struct Pref4 {
+  uint4 w0, w1, w2, w3;
+};
+__device__ __forceinline__ Pref4 pref_load4(const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  static_assert(kStageBytes == 4096, "pref_load4 holds a 4 KiB span");
+  const uint8_t* base = src + lo16;
+  const uint32_t n = (uint32_t)(hi - lo16), o = lane * 16u;
+  // (loads past the span re-read its first line)
+  Pref4 p;
+  p.w0 = *reinterpret_cast<const uint4*>(base + (o < n ? o : 0u));
+  p.w1 = *reinterpret_cast<const uint4*>(base + (o + 1024u < n ? o + 1024u : 0u));
+  p.w2 = *reinterpret_cast<const uint4*>(base + (o + 2048u < n ? o + 2048u : 0u));
+  p.w3 = *reinterpret_cast<const uint4*>(base + (o + 3072u < n ? o + 3072u : 0u));
+  return p;
+}
+__device__ __forceinline__ void pref_store4(const Pref4& p, uint8_t* dst, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  const uint32_t n = (uint32_t)(hi - lo16), o = lane * 16u;
+  if (o < n) *reinterpret_cast<uint4*>(dst + o) = p.w0;
+  if (o + 1024u < n) *reinterpret_cast<uint4*>(dst + o + 1024u) = p.w1;
+  if (o + 2048u < n) *reinterpret_cast<uint4*>(dst + o + 2048u) = p.w2;
+  if (o + 3072u < n) *reinterpret_cast<uint4*>(dst + o + 3072u) = p.w3;
+}
+
 // Lane-per-record FAST path. Each wave copies the contiguous span of its 64 records into its LDS
 // stage, then every lane checks its record's framing + CRC and runs the single-pass canonical walker
 // (fast_walk). Records the fast walker does not accept (non-canonical, erroneous, unknown keys), records
@@ -1562,8 +1739,9 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
-  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneBlock / 64) * 64u : 0u);  // templates
-  uint32_t* spec_l = tpl_l + sc.n_tpl * kTplWords;  // MODE 0: DevSchema::spec
+  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneBlock / 64) * 64u : 0u);
+  uint32_t* spec_l = tpl_l + (TFRG_TPL_SMEM ? 0u : sc.n_tpl * kTplWords);  // MODE 0: DevSchema::spec
+  uint32_t* spec_tl = spec_l + ((S + 7u) & ~7u);  // MODE 0: its targets (16-byte aligned)
   for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
   if constexpr (MODE == 1) {
     tsl[lane] = 0;
@@ -1572,11 +1750,15 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
-    for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneBlock) tpl_l[i] = sc.tpl[i];
+    if (!TFRG_TPL_SMEM)
+      for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneBlock) tpl_l[i] = sc.tpl[i];
   }
   const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
   if (spec_on)
-    for (uint32_t i = threadIdx.x; i < S; i += kLaneBlock) spec_l[i] = sc.spec[i];
+    for (uint32_t i = threadIdx.x; i < S; i += kLaneBlock) {
+      spec_l[i] = sc.spec[i];
+      spec_target(spec_tl + kSpecTgtWords * i, o, sc.spec[i], B.n);
+    }
   __syncthreads();
   const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
@@ -1590,16 +1772,49 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     nst = B.start[base + lane];
     nen = B.end[base + lane];
   }
+#if TFRG_LANE_PREF
+  // the first iteration's span in flight, and the next iteration's offsets
+  uint64_t cst = nst, cen = nen, plo16 = 0, phi = 0;
+  bool pstaged = lane_span(B, cst, cen, base + lane < B.n, fast_ok, lane_max, plo16, phi);
+  Pref4 pf{};
+  if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
+  nst = nen = 0;
+  if (base + lstride + lane < B.n) {
+    nst = B.start[base + lstride + lane];
+    nen = B.end[base + lstride + lane];
+  }
+#endif
   for (; base < B.n; base += lstride) {
     PHASE_MARK(p0);
     const uint64_t ri = base + lane;
     const bool valid = ri < B.n;
     const uint32_t r = (uint32_t)ri;
+#if TFRG_LANE_PREF
+    const uint64_t cst0 = cst, cen0 = cen;
+    const uint64_t lo16 = plo16;
+    const bool staged = pstaged;
+    if (staged) {
+      pref_store4(pf, stage, lo16, phi, lane);
+      wave_lds_sync();
+    }
+    {  // the next iteration's span: its loads in flight while this iteration decodes
+      const uint64_t rn = ri + lstride;
+      pstaged = lane_span(B, nst, nen, rn < B.n, fast_ok, lane_max, plo16, phi);
+      if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
+      cst = nst;
+      cen = nen;
+      if (rn + lstride < B.n) {
+        nst = B.start[rn + lstride];
+        nen = B.end[rn + lstride];
+      }
+    }
+#else
     const uint64_t cst0 = nst, cen0 = nen;
     if (ri + lstride < B.n) {
       nst = B.start[ri + lstride];
       nen = B.end[ri + lstride];
     }
+#endif
     RecView v{};
     bool mine = false;
     bool stg = false;  // counted by k_stage_count (staged large record, launched for this batch)
@@ -1620,6 +1835,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     }
     // wave-uniform staging decision over the span of this wave's records
     const bool span_rec = fast_ok && mine && v.status == TFRG_OK;
+#if !TFRG_LANE_PREF
     uint64_t lo, hi;
     wave_span(span_rec, v.st, v.e, lo, hi);
     const uint64_t lo16 = lo & ~15ull;
@@ -1628,6 +1844,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
+#endif
     PHASE_MARK(p1);
     PHASE_ADD(16, p0, p1);
     using SinkT = std::conditional_t<MODE == 1, MaskSink, CountSinkT<MODE == 0>>;
@@ -1639,7 +1856,11 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
                                 GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
         if constexpr (MODE == 0) {
           c.cnt = (lds_u32*)(cnt + threadIdx.x);
-          if (spec_on) c.spec = (const lds_u32*)spec_l;
+          if (spec_on) {
+            c.spec = (const lds_u32*)spec_l;
+            c.spec_t = (const lds_spec_t*)spec_tl;
+            c.spec_u = TFRG_TPL_SMEM ? sc.spec : spec_l;
+          }
         }
         return c;
       }
@@ -1649,20 +1870,23 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     if (staged && span_rec) {
       // a known record shape (template) first: it also carries most of the record's CRC-32C work
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-      uint32_t tcrc = 0;
       const bool fcrc = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
-      const int tm = sc.n_tpl ? tpl_match_crc<R>(fs, tpl_l, sc.n_tpl, T, fcrc, tcrc) : -1;
-      frame_verdicts<R, true>(B, v, T, stage, lo16, true, tm >= 0 ? tpl_l + (uint32_t)tm * kTplWords : nullptr, tcrc);
+#if TFRG_TPL_SMEM
+      const TplRef tg{(cu32*)sc.tpl};
+#else
+      const TplRef tg{tpl_l};
+#endif
+      TplHit th;
+      if (sc.n_tpl) th = tpl_match_u<R>(fs, true, tg, sc.n_tpl, T, fcrc);
+      frame_verdicts<R, true>(B, v, T, stage, lo16, true, &th);
       PHASE_MARK(p2);
       PHASE_ADD(17, p1, p2);
       sink.fast_reset(S);
-      if (strict_pass(B, v.verdict, true)) {  // (strict mode: a CRC failure is the slow kernel's)
-        if (tm >= 0) {  // a known record shape: its dict without the walk
-          tpl_put(fs, tpl_l + (uint32_t)tm * kTplWords, sink);
-          done = true;
-        } else {
-          done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
-        }
+      const bool pass = strict_pass(B, v.verdict, true);  // (strict mode: a CRC failure is the slow kernel's)
+      // a known record shape: its dict without the walk
+      if (sc.n_tpl) tpl_put_all(fs, pass, th.t, tg, sc.n_tpl, sink);
+      if (pass) {
+        done = th.t >= 0 || fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
         tried = true;
       }
       PHASE_MARK(p3);
@@ -1728,6 +1952,9 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
       if (done) {
         const size_t at = (size_t)k * B.n + r;
         o.order[at] = (uint16_t)ov;
+#ifdef TFRG_DIAG_NOCNT  // diagnostic build: no count word for regular speculatively placed values
+        if (!(spec_on && spec_l[k] && mine && c == (1u | kCountInline)))
+#endif
         o.count[at] = c;
       }
       const uint32_t x = c & ~kCountInline;
@@ -3781,8 +4008,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   const size_t keys_lds = fast_ok ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
-  const size_t tpl_lds = fast_ok ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (after the MODE 1 tile sums)
-  const size_t spec_lds = fast_ok && sc.spec ? r16(S * 4) : 0;               // (MODE 0 only)
+  const size_t tpl_lds = fast_ok && !TFRG_TPL_SMEM ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (TplRef)
+  // (MODE 0 only) spec words + their targets
+  const size_t spec_lds = fast_ok && sc.spec ? ((S + 7) & ~(size_t)7) * 4 + S * kSpecTgtWords * 4 : 0;
   const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + tpl_lds + spec_lds;
   // speculative placement only with the per-lane LDS dict (MODE 0); the later kernels see the same
   DevSchema scx = sc;

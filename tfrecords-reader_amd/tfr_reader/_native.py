@@ -72,6 +72,7 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_idx_load": (C.c_int, [C.c_char_p, C.POINTER(u64p), i64p]),
     "tfrg_free": (None, [C.c_void_p]),
     "tfrg_gather_ranges": (C.c_uint64, [C.c_void_p, u64p, u64p, C.c_int64, C.c_void_p]),
+    "tfrg_scan_keys": (C.c_int64, [C.c_void_p, C.c_uint64, u64p, u64p, C.c_int64, C.c_uint32, u64p, C.c_int64]),
     "tfrg_crc32c": (C.c_uint32, [C.c_void_p, C.c_uint64]),
     "tfrg_compression_of": (C.c_int, [C.c_void_p, C.c_uint64]),
     "tfrg_inflate": (C.c_int, [C.c_void_p, C.c_uint64, C.POINTER(u8p), u64p]),

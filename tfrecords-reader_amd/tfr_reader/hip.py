@@ -220,6 +220,24 @@ class HipDecoder:
             new |= self.keys.intern(bytes(buf[off : off + ln]), kind)
         return new
 
+    SEED_SAMPLE = 64  # records per host decode whose keys seed the key table (tfrg_scan_keys)
+
+    def _seed_keys(self, buf: np.ndarray, st: np.ndarray, en: np.ndarray, flags: int) -> None:
+        """Intern the keys of a sample of the batch's records before the device sees them, so a first
+        decode of a new schema does not send every record through the exact walker's miss pass."""
+        n = int(st.shape[0])
+        if n == 0 or buf.size == 0:
+            return
+        if n > self.SEED_SAMPLE:
+            pick = np.linspace(0, n - 1, self.SEED_SAMPLE).astype(np.int64)
+            st, en = np.ascontiguousarray(st[pick]), np.ascontiguousarray(en[pick])
+        cap = 256
+        out = np.zeros((cap, 3), np.uint64)
+        k = int(self._lib.tfrg_scan_keys(N.ptr(buf), buf.size, N.ptr(st, N.u64p), N.ptr(en, N.u64p), st.size,
+                                         flags & N.FLAG_PAYLOAD_ONLY, N.ptr(out, N.u64p), cap))
+        for off, ln, kind in out[:k].tolist():
+            self.keys.intern(bytes(buf[off : off + ln]), kind)
+
     def decode(
         self,
         buf,
@@ -246,6 +264,7 @@ class HipDecoder:
         n = int(st.shape[0])
         flags = self._flags(payload_only, crc, strict_crc, materialize_bytes)
         with self._lock:
+            self._seed_keys(buf, st, en, flags)
             # every round interns at least one new key (else it raises), and at most 65,536 miss
             # entries are reported per round, so high-cardinality key sets take several rounds
             while True:
@@ -486,6 +505,8 @@ class BatchResult:
                                                                       KIND_NAMES[self.slot_kind[s]] == kind)]
         if not slots:
             raise KeyError(key)
+        if len(slots) > 1:  # (the key table outlives batches: only the kinds present here count)
+            slots = [s for s in slots if self.order[s].any()] or slots[:1]
         if len(slots) > 1:
             raise ValueError(f"key {key!r} has several kinds in this batch; pass kind=")
         s = slots[0]
