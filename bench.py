@@ -210,10 +210,11 @@ def _check(infos) -> None:
         assert info.n_errors == 0 and info.n_miss_records == 0 and info.scan_timeout == 0, "decode check failed"
 
 
-def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> dict:
+def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, templates: bool = True) -> dict:
     """Decode the rank's resident shard `steps` times. The shard is cut into record-range batches
     of <= --batch-bytes (tfr_reader.shard.plan_batches), batch k decoded by its own context on
-    stream k % --streams; a step is the decode of every batch."""
+    stream k % --streams; a step is the decode of every batch. templates=False: no record-shape
+    templates (every lane record takes the canonical walk; results identical)."""
     from tfr_reader import hip, shard
 
     dev, main = ctx.dev, ctx.stream
@@ -226,6 +227,9 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int) -> 
     d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
     d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
     del rst, ren
+    if not templates:
+        for d in sd._decoders(len(plan)):
+            d.set_templates(False)
     sd.learn(plan, w.buf, w.starts, w.ends)
     present = _present_lists(sd.decs[0], w)
     side = [torch.cuda.Stream(dev) for _ in range(max(1, ctx.args.streams))]
@@ -482,6 +486,7 @@ def run(args) -> None:
         cpu = cpu_baseline(w, args.cpu_seconds)
 
     configs = {}
+    templates_off = None
     if world == 1 and only is None and not args.no_extra:
         del w
         # c4of8: one rank's share of the same directory at N = 8 (32 of 256 files) decoded alone, the
@@ -495,6 +500,13 @@ def run(args) -> None:
                 cw = single_workload(name)
             m = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps)
             del m["_d_bytes"], m["_elapsed"]
+            if name == "c4of8":  # the same share without record-shape templates (canonical walk only)
+                t = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps, templates=False)
+                templates_off = {"workload": "c4of8", "ms_per_step": t["ms_per_step"], "GiB_s": t["GiB_s"],
+                                 "k_lane_count_ms": t["kernels_ms"].get("k_lane_count"),
+                                 "templates_on_ms_per_step": m["ms_per_step"],
+                                 "templates_on_k_lane_count_ms": m["kernels_ms"].get("k_lane_count")}
+                del t
             if hasattr(cw, "files_mine"):
                 m["files"] = cw.files_mine
             if not args.no_cpu:
@@ -544,6 +556,8 @@ def run(args) -> None:
             if "c4of8" in configs:
                 line["weak_scaling"] = {"files_per_gpu": configs["c4of8"]["files"], "GiB_s_per_gpu": configs["c4of8"]["GiB_s"],
                                         "note": "rank 0's LPT share of the 256 files at N = 8, decoded alone"}
+        if templates_off:
+            line["templates_off"] = templates_off
         print(json.dumps(line), flush=True)
     if dist:
         tdist.destroy_process_group()

@@ -1,0 +1,101 @@
+"""The headline path at its full size (BASELINE.json configs[4], bench.py's N = 8 per-GPU share):
+rank 0's LPT share of the 256-file C1-shaped directory (32 files, ~16.8 M records, ~0.99 GB)
+resident in HBM, decoded exactly as bench.py times it (key table and record-shape templates learned
+from a 4,096-record host sample, ShardDecoder.decode_device over two streams), then every value
+checked against what the deterministic generator wrote, record by record, vectorised:
+
+* status OK and verdict 7 (length field, length CRC and payload CRC all match) for every record;
+* the dict order of every record: ``label`` first, ``id`` second (reader order, decoder.pyx:107-199);
+* the ``label`` int64 column = (i mod 1000) per file, its row splits = 0..n;
+* the ``id`` bytes_list column: one 12-byte element per record whose bytes in the image are
+  ``img-%08d`` of (f * 1,000,003 + i) mod 10^8 (synth.c1_blob).
+
+The generator is pinned to the reference encoder byte for byte (tests/test_synth.py), and the small
+C1 shapes to the oracle (test_gpu_parity.py, test_c4_gpu.py); this test covers the size the bench
+line is quoted on, where the oracle itself would take minutes.
+"""
+
+import numpy as np
+import pytest
+
+from tfr_reader import shard, synth
+
+pytestmark = pytest.mark.gpu
+
+N_FILES, WORLD = 256, 8
+
+
+def _expected_ids(f: int, n: int, lo: int, hi: int) -> np.ndarray:
+    x = (f * 1_000_003 + np.arange(lo, hi, dtype=np.int64)) % 10**8
+    out = np.empty((hi - lo, 12), np.uint8)
+    out[:, :4] = np.frombuffer(b"img-", np.uint8)
+    for k in range(8):
+        out[:, 11 - k] = 48 + (x // 10**k) % 10
+    return out
+
+
+def test_headline_share_full_size_values():
+    import torch
+
+    sizes = synth.c4_file_sizes(N_FILES, "c1")
+    mine = shard.lpt_partition(sizes, WORLD)[0]
+    imgs = [synth.c4_file(f, "c1") for f in mine]
+    sb = shard.ShardBatch([synth.c4_file_name(f) for f in mine], imgs)
+    del imgs
+    n = len(sb)
+    assert n > 15_000_000
+    dev = torch.device("cuda", 0)
+    sd = shard.ShardDecoder(0)
+    try:
+        plan = sd.plan(sb.starts, sb.ends, sb.nbytes)
+        rst, ren = sd.rebase(plan, sb.starts, sb.ends)
+        d_bytes = torch.zeros(((sb.nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
+        d_bytes[: sb.nbytes].copy_(torch.from_numpy(sb.buf))
+        d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
+        d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        sd.learn(plan, sb.buf, sb.starts, sb.ends)
+        assert all(d.template_count() >= 1 for d in sd.decs)
+        streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
+        sd.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(),
+                         streams=[s.cuda_stream for s in streams])
+        infos = sd.infos(plan)
+        assert not any(i.n_miss_records or i.n_errors for i in infos)
+        res = sd.fetch(plan, sb.buf, sb.starts, sb.ends)
+    finally:
+        sd.close()
+    assert len(res) == n
+    assert (res.status == 0).all()
+    assert (res.verdict == 7).all()
+    # expected values, per file: record i of file f has label i % 1000 and id img-%08d(f*1000003+i)
+    file_idx = np.asarray(mine)[sb.file_of]
+    rec_in_file = np.arange(n, dtype=np.int64) - sb.file_first[sb.file_of]
+    checked = 0
+    for r0, r1, r in res.parts:
+        kl = [s for s, k in enumerate(r.slot_key) if k == "label" and r.slot_kind[s] == 3]
+        ki = [s for s, k in enumerate(r.slot_key) if k == "id" and r.slot_kind[s] == 1]
+        assert len(kl) == 1 and len(ki) == 1
+        sl, si = kl[0], ki[0]
+        assert (r.order[sl] == 1).all() and (r.order[si] == 2).all()
+        m = r1 - r0
+        for s in (sl, si):
+            rs = r.row_splits[s].astype(np.int64)
+            assert (rs - rs[0] == np.arange(m + 1)).all()
+        lab_base = int(r.slot_base[sl]) + int(r.row_splits[sl][0])
+        labels = r.i64[lab_base : lab_base + m]
+        assert np.array_equal(labels, rec_in_file[r0:r1] % 1000)
+        id_base = int(r.slot_base[si]) + int(r.row_splits[si][0])
+        lens = r.bytes_len[id_base : id_base + m]
+        offs = r.bytes_off[id_base : id_base + m].astype(np.int64)
+        assert (lens == 12).all()
+        for c0 in range(0, m, 1 << 20):  # bytes of the views, in 1 M-record chunks
+            c1 = min(m, c0 + (1 << 20))
+            got = r.buf[offs[c0:c1, None] + np.arange(12)]
+            fr = file_idx[r0 + c0 : r0 + c1]
+            want = np.empty_like(got)
+            for f in np.unique(fr):
+                sel = np.nonzero(fr == f)[0]
+                i0 = int(rec_in_file[r0 + c0 + sel[0]])
+                want[sel] = _expected_ids(int(f), 0, i0, i0 + sel.size)
+            assert np.array_equal(got, want), (r0, c0)
+        checked += m
+    assert checked == n

@@ -773,6 +773,10 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // Kernels
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
+#ifndef TFRG_LANE_BLOCK
+#define TFRG_LANE_BLOCK 256
+#endif
+constexpr int kLaneCountBlock = TFRG_LANE_BLOCK;  // k_lane_count workgroup (its LDS tables are per workgroup)
 #ifndef TFRG_LANE_MINB
 #define TFRG_LANE_MINB 6  // waves per SIMD the (LDS-dict) count kernel is register-budgeted for
 #endif
@@ -1150,6 +1154,10 @@ __device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e,
 // round trips; four blocks per round would cost the staged path its occupancy in VGPRs)
 template <bool WIN>
 __device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o, uint32_t e, uint32_t& cnt) {
+#ifdef TFRG_DIAG_NOCOUNT  // diagnostic build (timing only, wrong counts): no loads of packed bodies
+  cnt = (e - o) >> 2;
+  return true;
+#endif
   uint32_t run = 0, terms = 0;
   const uint64_t a0 = s.base + o, a1 = s.base + e;
   const uint64_t lb = s.lim - 12;  // last readable 16-byte block
@@ -1664,8 +1672,9 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 }
 
 #ifndef TFRG_LANE_PREF
-#define TFRG_LANE_PREF 0
+#define TFRG_LANE_PREF 0  // lane kernel staging: 0 synchronous, 1 next span in registers, 2 next span by LDS-DMA
 #endif
+constexpr uint32_t kLaneBufs = TFRG_LANE_PREF == 2 ? 2u : 1u;  // stages per wave
 // The lane kernel's staging decision for one wave's records, from their offsets alone: the span of
 // the records the lane walk takes (fast path, <= lane_max), staged when it fits kStageBytes.
 __device__ __forceinline__ bool lane_span(const DevBatch& B, uint64_t st, uint64_t en, bool valid, bool fast_ok,
@@ -1711,6 +1720,35 @@ __device__ __forceinline__ void pref_store4(const Pref4& p, uint8_t* dst, uint64
   if (o + 3072u < n) *reinterpret_cast<uint4*>(dst + o + 3072u) = p.w3;
 }
 
+// LDS byte address of a pointer into shared memory
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
+// Copies absolute bytes [lo16, hi) (hi - lo16 <= kStageBytes) into the stage dst by LDS-DMA:
+// global_load_lds_dwordx4 writes lane l's 16 bytes at M0 + 16 l, one 1 KiB piece per
+// wave-instruction, with no VGPR destination. Lanes past the span re-read the piece's first line
+// (their bytes land past the span, inside the stage). The loads are inline asm, outside the
+// compiler's s_waitcnt bookkeeping: the caller waits vmcnt(0) before reading dst (an asm load
+// only ever makes the compiler's own in-order vmcnt waits stricter).
+__device__ __forceinline__ void dma_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
+  const uint32_t n = rfl32((uint32_t)(hi - lo16));
+  const uint8_t* base = src + rfl64(lo16);
+  const uint32_t d0 = rfl32(lds_addr(dst));
+  for (uint32_t k = 0; k < n; k += 1024u) {  // (wave-uniform)
+    const uint32_t off = k + lane * 16u;
+    const uint8_t* g = base + (off < n ? off : k);
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(d0 + k)
+        : "memory");
+  }
+}
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
 // Lane-per-record FAST path. Each wave copies the contiguous span of its 64 records into its LDS
 // stage, then every lane checks its record's framing + CRC and runs the single-pass canonical walker
 // (fast_walk). Records the fast walker does not accept (non-canonical, erroneous, unknown keys), records
@@ -1720,42 +1758,43 @@ __device__ __forceinline__ void pref_store4(const Pref4& p, uint8_t* dst, uint64
 // GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
 // MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
 template <int R, bool COMPAT, int MODE>
-__global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+__global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                            const uint32_t* __restrict__ crc_tab,
                                                                            uint32_t lane_max, uint32_t wave_stage,
                                                                            uint32_t stage_cnt) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // slicing tables at a static LDS address: lookups fold the table base into the ds_read offset
   __shared__ uint32_t tab[256 * kLaneSlice * R];
-  uint32_t* cnt = lds;                                       // [n_slots][kLaneBlock]
+  uint32_t* cnt = lds;                                       // [n_slots][kLaneCountBlock]
   constexpr bool GORD = MODE != 0;  // no per-lane LDS dict
   const uint32_t S = sc.n_slots;
-  const uint32_t cnt_words = GORD ? 0u : S * kLaneBlock;
-  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneBlock]
-  const uint32_t ord_bytes = GORD ? 0u : ((S * kLaneBlock * 2u + 15u) & ~15u);
+  const uint32_t cnt_words = GORD ? 0u : S * kLaneCountBlock;
+  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneCountBlock]
+  const uint32_t ord_bytes = GORD ? 0u : ((S * kLaneCountBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage_all = reinterpret_cast<uint8_t*>(ord) + ord_bytes;
-  uint8_t* stage = stage_all + wib * kStageStride;
-  uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneBlock / 64) * kStageStride);
+  // (TFRG_LANE_PREF 2: two stages per wave, the next span's LDS-DMA lands in the other one)
+  uint8_t* stage_w = stage_all + wib * kLaneBufs * kStageStride;
+  uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneCountBlock / 64) * kLaneBufs * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
-  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneBlock / 64) * 64u : 0u);
+  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneCountBlock / 64) * 64u : 0u);
   uint32_t* spec_l = tpl_l + (TFRG_TPL_SMEM ? 0u : sc.n_tpl * kTplWords);  // MODE 0: DevSchema::spec
   uint32_t* spec_tl = spec_l + ((S + 7u) & ~7u);  // MODE 0: its targets (16-byte aligned)
-  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneBlock) tab[i] = crc_tab[2048 + i / R];
+  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneCountBlock) tab[i] = crc_tab[2048 + i / R];
   if constexpr (MODE == 1) {
     tsl[lane] = 0;
   }
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
   if (fast_ok) {
-    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneBlock) kht[i] = sc.ht[i];
-    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneBlock) krec[i] = sc.krec[i];
+    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneCountBlock) kht[i] = sc.ht[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneCountBlock) krec[i] = sc.krec[i];
     if (!TFRG_TPL_SMEM)
-      for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneBlock) tpl_l[i] = sc.tpl[i];
+      for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneCountBlock) tpl_l[i] = sc.tpl[i];
   }
   const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
   if (spec_on)
-    for (uint32_t i = threadIdx.x; i < S; i += kLaneBlock) {
+    for (uint32_t i = threadIdx.x; i < S; i += kLaneCountBlock) {
       spec_l[i] = sc.spec[i];
       spec_target(spec_tl + kSpecTgtWords * i, o, sc.spec[i], B.n);
     }
@@ -1765,8 +1804,8 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
 
   // the next iteration's offsets are requested before this iteration's stores (one HBM round trip
   // less on the critical path of the next iteration)
-  const uint64_t lstride = (uint64_t)gridDim.x * kLaneBlock;
-  uint64_t base = (uint64_t)blockIdx.x * kLaneBlock + wib * 64u;
+  const uint64_t lstride = (uint64_t)gridDim.x * kLaneCountBlock;
+  uint64_t base = (uint64_t)blockIdx.x * kLaneCountBlock + wib * 64u;
   uint64_t nst = 0, nen = 0;
   if (base + lane < B.n) {
     nst = B.start[base + lane];
@@ -1776,8 +1815,13 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
   // the first iteration's span in flight, and the next iteration's offsets
   uint64_t cst = nst, cen = nen, plo16 = 0, phi = 0;
   bool pstaged = lane_span(B, cst, cen, base + lane < B.n, fast_ok, lane_max, plo16, phi);
+#if TFRG_LANE_PREF == 2
+  uint32_t buf = 0;
+  if (pstaged) dma_span(stage_w, B.bytes, plo16, phi, lane);
+#else
   Pref4 pf{};
   if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
+#endif
   nst = nen = 0;
   if (base + lstride + lane < B.n) {
     nst = B.start[base + lstride + lane];
@@ -1793,14 +1837,30 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     const uint64_t cst0 = cst, cen0 = cen;
     const uint64_t lo16 = plo16;
     const bool staged = pstaged;
+#if TFRG_LANE_PREF == 2
+    // this span's DMA (issued one iteration ago) and the offsets loaded with it have landed; the
+    // wait also covers the previous iteration's stores (one counter)
+    wait_vm0();
+    uint8_t* stage = stage_w + buf * kStageStride;
+#else
+    uint8_t* stage = stage_w;
     if (staged) {
       pref_store4(pf, stage, lo16, phi, lane);
       wave_lds_sync();
     }
+#endif
     {  // the next iteration's span: its loads in flight while this iteration decodes
       const uint64_t rn = ri + lstride;
       pstaged = lane_span(B, nst, nen, rn < B.n, fast_ok, lane_max, plo16, phi);
+#if TFRG_LANE_PREF == 2
+      if (pstaged) {
+        wait_lgkm0();  // (the other stage's last reads, one iteration ago, are complete)
+        dma_span(stage_w + (buf ^ 1u) * kStageStride, B.bytes, plo16, phi, lane);
+      }
+      buf ^= 1u;
+#else
       if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
+#endif
       cst = nst;
       cen = nen;
       if (rn + lstride < B.n) {
@@ -1836,6 +1896,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
     // wave-uniform staging decision over the span of this wave's records
     const bool span_rec = fast_ok && mine && v.status == TFRG_OK;
 #if !TFRG_LANE_PREF
+    uint8_t* stage = stage_w;
     uint64_t lo, hi;
     wave_span(span_rec, v.st, v.e, lo, hi);
     const uint64_t lo16 = lo & ~15ull;
@@ -1853,7 +1914,7 @@ __global__ __launch_bounds__(kLaneBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_
         return MaskSink{&o, B.n, r, tsl};
       } else {
         CountSinkT<MODE == 0> c{&sc, &o, dict_ord<MODE == 0>(o.order + r, ord + threadIdx.x),
-                                GORD ? B.n : (uint32_t)kLaneBlock, 0, B.n, r, v.p0, false, true};
+                                GORD ? B.n : (uint32_t)kLaneCountBlock, 0, B.n, r, v.p0, false, true};
         if constexpr (MODE == 0) {
           c.cnt = (lds_u32*)(cnt + threadIdx.x);
           if (spec_on) {
@@ -2083,8 +2144,8 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
 // the slices of a record split over waves XOR together in crc_part (CRC-32C is linear, crc32c.h)
 // and the wave whose rounds complete the record finishes it.
 constexpr int kCrcDepth = TFRG_CRC_DEPTH;
-constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
-constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
+[[maybe_unused]] constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
+[[maybe_unused]] constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
 constexpr uint32_t kPowTabOff = 26624;   // crc_tab: [24][4][256] multiply by x^(8192 * 2^k) (split-slice shifts)
 constexpr uint32_t kNumCst = 128;
 
@@ -3356,96 +3417,118 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
   const uint32_t S = sc.n_slots;
   if (blockIdx.x == 0)
     for (uint32_t k = threadIdx.x; k < S; k += kLaneBlock) o.rs[(size_t)k * (B.n + 1) + B.n] = o.totals[k];
-  const uint32_t tile0 = blockIdx.x * kDT;
-  uint32_t r[kDT];
-  bool valid[kDT];
-#pragma unroll
-  for (uint32_t t = 0; t < kDT; ++t) {
-    r[t] = ((tile0 + t) << kTileShift) + threadIdx.x;
-    valid[t] = r[t] < B.n;
+  // slots whose speculative placement by the lane kernel is final (DevSchema::spec): nothing to do.
+  // Read once (the first 64 slots as a mask): the tile-sum stores below may alias irr for the
+  // compiler, which would otherwise re-load spec / irr with their latency in every group.
+  uint64_t pmask = 0;
+  if (sc.spec)
+    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;
+  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) |
+          __builtin_amdgcn_readfirstlane((uint32_t)pmask);
+  auto placed = [&](uint32_t k) -> bool {
+    return k < 64u ? ((pmask >> k) & 1ull) != 0ull : k < S && spec_placed(sc.spec, o, k);
+  };
+  if (S <= 64u && pmask == (~0ull >> (64u - S))) {  // every slot placed: only the scan words to clear
+    const size_t nz = (size_t)S * o.tile_stride;
+    for (size_t i = (size_t)blockIdx.x * kLaneBlock + threadIdx.x; i < nz; i += (size_t)gridDim.x * kLaneBlock)
+      o.tsum[i] = 0u;
+    if (blockIdx.x == 0)
+      for (uint32_t i = threadIdx.x; i < 2u * S * o.n_chunks; i += kLaneBlock) reinterpret_cast<uint32_t*>(o.spine_lb)[i] = 0u;
+    return;
   }
-  // row splits of every slot + inline single values. A non-zero count implies a decoded record
-  // with the slot present (failed records and absent slots have count 0).
-  uint32_t need = 0;  // bit t: record r[t] has an out-of-line list
   uint32_t buf = 0;
-  // slots whose speculative placement by the lane kernel is final (DevSchema::spec): nothing to do
-  auto placed = [&](uint32_t k) -> bool { return k < S && spec_placed(sc.spec, o, k); };
-  for (uint32_t k0 = 0; k0 < S; k0 += kDG) {
-    bool sk[kDG];
-    bool all = true;
-#pragma unroll
-    for (uint32_t g = 0; g < kDG; ++g) {
-      sk[g] = placed(k0 + g);
-      all &= sk[g] || k0 + g >= S;
-    }
-    if (all) continue;  // (workgroup-uniform; buf toggles only with a barrier)
-    uint32_t c[kDT][kDG], ex[kDT][kDG];
-    uint2 lc[kDT][kDG];
-#pragma unroll
-    for (uint32_t t = 0; t < kDT; ++t) {  // every load of the group issued before the barrier
-#pragma unroll
-      for (uint32_t g = 0; g < kDG; ++g) {
-        const uint32_t k = k0 + g < S ? k0 + g : k0;
-        const bool in = valid[t] && k0 + g < S && !sk[g];
-        c[t][g] = in ? o.count[(size_t)k * B.n + r[t]] : 0u;
-        lc[t][g] = in ? o.loc[(size_t)k * B.n + r[t]] : make_uint2(0, 0);
-      }
-    }
-#pragma unroll
+  // a resident grid strides over the groups of kDT tiles (a launch of one workgroup per group spent
+  // most of its time dispatching workgroups that only zero their tile sums when every slot is placed)
+  const uint32_t n_groups = (n_tiles + kDT - 1) / kDT;
+  for (uint32_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {  // (workgroup-uniform)
+    const uint32_t tile0 = grp * kDT;
+    uint32_t r[kDT];
+    bool valid[kDT];
+  #pragma unroll
     for (uint32_t t = 0; t < kDT; ++t) {
-#pragma unroll
+      r[t] = ((tile0 + t) << kTileShift) + threadIdx.x;
+      valid[t] = r[t] < B.n;
+    }
+    // row splits of every slot + inline single values. A non-zero count implies a decoded record
+    // with the slot present (failed records and absent slots have count 0).
+    uint32_t need = 0;  // bit t: record r[t] has an out-of-line list
+    for (uint32_t k0 = 0; k0 < S; k0 += kDG) {
+      bool sk[kDG];
+      bool all = true;
+  #pragma unroll
       for (uint32_t g = 0; g < kDG; ++g) {
-        const uint32_t x = c[t][g] & ~kCountInline;
-        // 0/1 counts (single values): the inclusive scan is a masked popcount of the ballot
-        const uint32_t incl = __ballot(x > 1u) ? wave_incl_scan_u32(x, lane)
-                                               : (uint32_t)__popcll(__ballot(x != 0u) & (~0ull >> (63u - lane)));
-        ex[t][g] = incl - x;
-        if (lane == 63) s_w[buf][t * kDG + g][wib] = incl;
+        sk[g] = placed(k0 + g);
+        all &= sk[g] || k0 + g >= S;
       }
-    }
-    __syncthreads();  // (the other buffer is rewritten only after the next group's barrier)
-#pragma unroll
-    for (uint32_t g = 0; g < kDG; ++g) {
-      const uint32_t k = k0 + g;
-      if (k >= S) break;
-      if (sk[g]) continue;
-      const uint32_t kind = sc.slot_kind[k];
-      const uint64_t sbase = o.slot_base[k];
-#pragma unroll
+      if (all) continue;  // (workgroup-uniform; buf toggles only with a barrier)
+      uint32_t c[kDT][kDG], ex[kDT][kDG];
+      uint2 lc[kDT][kDG];
+  #pragma unroll
+      for (uint32_t t = 0; t < kDT; ++t) {  // every load of the group issued before the barrier
+  #pragma unroll
+        for (uint32_t g = 0; g < kDG; ++g) {
+          const uint32_t k = k0 + g < S ? k0 + g : k0;
+          const bool in = valid[t] && k0 + g < S && !sk[g];
+          c[t][g] = in ? o.count[(size_t)k * B.n + r[t]] : 0u;
+          lc[t][g] = in ? o.loc[(size_t)k * B.n + r[t]] : make_uint2(0, 0);
+        }
+      }
+  #pragma unroll
       for (uint32_t t = 0; t < kDT; ++t) {
-        if (tile0 + t >= n_tiles) break;
-        uint32_t pre = o.tsum[(size_t)k * o.tile_stride + tile0 + t];
-        for (uint32_t w = 0; w < wib; ++w) pre += s_w[buf][t * kDG + g][w];
-        const uint32_t rsv = pre + ex[t][g];
-        if (valid[t]) o.rs[(size_t)k * (B.n + 1) + r[t]] = rsv;
-        if (c[t][g] & kCountInline) put_inline(o, kind, lc[t][g], sbase + rsv);
-        else if (c[t][g]) need |= 1u << t;
+  #pragma unroll
+        for (uint32_t g = 0; g < kDG; ++g) {
+          const uint32_t x = c[t][g] & ~kCountInline;
+          // 0/1 counts (single values): the inclusive scan is a masked popcount of the ballot
+          const uint32_t incl = __ballot(x > 1u) ? wave_incl_scan_u32(x, lane)
+                                                 : (uint32_t)__popcll(__ballot(x != 0u) & (~0ull >> (63u - lane)));
+          ex[t][g] = incl - x;
+          if (lane == 63) s_w[buf][t * kDG + g][wib] = incl;
+        }
+      }
+      __syncthreads();  // (the other buffer is rewritten only after the next group's barrier)
+  #pragma unroll
+      for (uint32_t g = 0; g < kDG; ++g) {
+        const uint32_t k = k0 + g;
+        if (k >= S) break;
+        if (sk[g]) continue;
+        const uint32_t kind = sc.slot_kind[k];
+        const uint64_t sbase = o.slot_base[k];
+  #pragma unroll
+        for (uint32_t t = 0; t < kDT; ++t) {
+          if (tile0 + t >= n_tiles) break;
+          uint32_t pre = o.tsum[(size_t)k * o.tile_stride + tile0 + t];
+          for (uint32_t w = 0; w < wib; ++w) pre += s_w[buf][t * kDG + g][w];
+          const uint32_t rsv = pre + ex[t][g];
+          if (valid[t]) o.rs[(size_t)k * (B.n + 1) + r[t]] = rsv;
+          if (c[t][g] & kCountInline) put_inline(o, kind, lc[t][g], sbase + rsv);
+          else if (c[t][g]) need |= 1u << t;
+        }
+      }
+      buf ^= 1u;
+    }
+    // records with an out-of-line list: k_list_gather (kept out of this kernel so its register
+    // budget stays that of the scan); larger records are skipped there (wavefront gathers)
+  #pragma unroll
+    for (uint32_t t = 0; t < kDT; ++t) {
+      const bool nd = (need >> t) & 1u;
+      const uint64_t nm = __ballot(nd);
+      if (nm) {
+        const int f = __builtin_ctzll(nm);
+        uint32_t b0 = 0;
+        if (lane == (uint32_t)f) b0 = atomicAdd(&o.info[kInfoNeed], (uint32_t)__popcll(nm));
+        b0 = __shfl(b0, f, 64);
+        if (nd) o.slow_list[b0 + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull))] = r[t];
       }
     }
-    buf ^= 1u;
+    // Leave the scan words zeroed for the next decode (no per-call memset): this group's tile
+    // prefixes of every slot (+ the stride padding after the last tile), and the spine's look-back
+    // words (workgroup 0; k_spine has finished).
+    __syncthreads();
+    const uint32_t t_end = tile0 + kDT < n_tiles ? tile0 + kDT : (tile0 < n_tiles ? o.tile_stride : tile0);
+    const uint32_t span = t_end - tile0;
+    for (uint32_t i = threadIdx.x; i < S * span; i += kLaneBlock)
+      o.tsum[(size_t)(i / span) * o.tile_stride + tile0 + i % span] = 0u;
   }
-  // records with an out-of-line list: k_list_gather (kept out of this kernel so its register
-  // budget stays that of the scan); larger records are skipped there (wavefront gathers)
-#pragma unroll
-  for (uint32_t t = 0; t < kDT; ++t) {
-    const bool nd = (need >> t) & 1u;
-    const uint64_t nm = __ballot(nd);
-    if (nm) {
-      const int f = __builtin_ctzll(nm);
-      uint32_t b0 = 0;
-      if (lane == (uint32_t)f) b0 = atomicAdd(&o.info[kInfoNeed], (uint32_t)__popcll(nm));
-      b0 = __shfl(b0, f, 64);
-      if (nd) o.slow_list[b0 + (uint32_t)__popcll(nm & ((1ull << lane) - 1ull))] = r[t];
-    }
-  }
-  // Leave the scan words zeroed for the next decode (no per-call memset): this workgroup's tile
-  // prefixes of every slot (+ the stride padding after the last tile), and the spine's look-back
-  // words (workgroup 0; k_spine has finished).
-  __syncthreads();
-  const uint32_t t_end = tile0 + kDT < n_tiles ? tile0 + kDT : (tile0 < n_tiles ? o.tile_stride : tile0);
-  const uint32_t span = t_end - tile0;
-  for (uint32_t i = threadIdx.x; i < S * span; i += kLaneBlock)
-    o.tsum[(size_t)(i / span) * o.tile_stride + tile0 + i % span] = 0u;
   if (blockIdx.x == 0)
     for (uint32_t i = threadIdx.x; i < 2u * S * o.n_chunks; i += kLaneBlock) reinterpret_cast<uint32_t*>(o.spine_lb)[i] = 0u;
 }
@@ -3988,7 +4071,10 @@ __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchem
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (slice-by-8: 8 KiB per copy)
 
-constexpr size_t kLaneLdsBudget = 64 * 1024;  // lane kernels (occupancy): likewise
+#ifndef TFRG_LANE_LDS_BUDGET
+#define TFRG_LANE_LDS_BUDGET (64 * 1024)
+#endif
+constexpr size_t kLaneLdsBudget = TFRG_LANE_LDS_BUDGET;  // lane kernels (occupancy): likewise
 
 const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_stage_count", "k_tail_count", "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
@@ -4003,9 +4089,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   };
   const size_t S = sc.n_slots;
   const uint32_t n_tiles = (b.n + kTileRecs - 1) / kTileRecs;
-  const size_t dict_lane = S * kLaneBlock * 4 + r16(S * kLaneBlock * 2);  // cnt u32 + ord u16 per lane
+  const size_t dict_lane = S * kLaneCountBlock * 4 + r16(S * kLaneCountBlock * 2);  // cnt u32 + ord u16 per lane
   const size_t tab_lds = 256ull * kLaneSlice * kLaneRep * 4;
-  const size_t stage_lds = (size_t)kStageStride * (kLaneBlock / 64);
+  const size_t stage_lds = (size_t)kStageStride * kLaneBufs * (kLaneCountBlock / 64);
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   const size_t keys_lds = fast_ok ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
   const size_t tpl_lds = fast_ok && !TFRG_TPL_SMEM ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (TplRef)
@@ -4023,24 +4109,25 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // one round of resident workgroups (a second, partial round would idle most CUs at the tail)
   auto resident_grid = [&](const void* fn, size_t lds, bool cap = true) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLaneBlock, lds) != hipSuccess || per_cu < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLaneCountBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus;
-    return g < cfg.lane_grid || !cap ? g : cfg.lane_grid;
+    const int need = (int)(((int64_t)cfg.lane_grid * 256 + kLaneCountBlock - 1) / kLaneCountBlock);
+    return g < need || !cap ? g : need;
   };
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
-                       dim3(kLaneBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
+                       dim3(kLaneCountBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
   } else if (S <= 64) {
-    const size_t lds = stage_lds + keys_lds + (kLaneBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
+    const size_t lds = stage_lds + keys_lds + (kLaneCountBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
                        st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
   } else {
     const size_t lds = stage_lds + keys_lds + tpl_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
-    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneBlock), lds,
+    hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
                        st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
   }
   mark(kStageStageCount);
@@ -4080,12 +4167,16 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        scx.spec, b.n);
   mark(kStageDownGather);
   if (S > 0) {
-    if (n_tiles >= 16u * (uint32_t)cfg.num_cus)
-      hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3((n_tiles + 3) / 4), dim3(kLaneBlock), 0, st, b, scx, o,
-                         cfg.lane_max, n_tiles);
-    else
-      hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles), dim3(kLaneBlock), 0, st, b, scx, o, cfg.lane_max,
-                         n_tiles);
+    // (at most 8 resident 256-thread workgroups per CU; larger batches stride)
+    const uint32_t resident = 8u * (uint32_t)cfg.num_cus;
+    if (n_tiles >= 16u * (uint32_t)cfg.num_cus) {
+      const uint32_t ng = (n_tiles + 3) / 4;
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3(ng < resident ? ng : resident), dim3(kLaneBlock), 0, st, b,
+                         scx, o, cfg.lane_max, n_tiles);
+    } else {
+      hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles < resident ? n_tiles : resident), dim3(kLaneBlock),
+                         0, st, b, scx, o, cfg.lane_max, n_tiles);
+    }
   }
   mark(kStageTailGather);
   if (S > 0) {  // the gathers after the scan: lane records' lists, staged and huge large records
