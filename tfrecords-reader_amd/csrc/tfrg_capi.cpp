@@ -81,6 +81,7 @@ struct tfrg_ctx {
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
   DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum, crc_rec, crc_base, crc_part;
+  DBuf dq, dq_cnt;  // deferred packed-int64 bodies (k_body_count)
   DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
   bool materialized = false;
   bool tsum_dirty = true;  // the scan words must be cleared before the next decode
@@ -183,7 +184,8 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
-                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec};
+                 &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec,
+                 &c->dq, &c->dq_cnt};
   for (DBuf* b : all) b->release();
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
@@ -629,6 +631,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   // fresh buffer, or one a failed launch may have left dirty, is cleared here
   if (c->tsum.cap != tsum_cap0 || c->tsum_dirty) {
     HIP_TRY(hipMemsetAsync(c->tsum.p, 0, c->tsum.cap, st));
+    // (no stale kStatusRedo: a decode whose launches failed may have left one)
+    HIP_TRY(hipMemsetAsync(c->status.p, 0, c->status.cap, st));
     c->tsum_dirty = false;
   }
   if (S && n == 0) HIP_TRY(hipMemsetAsync(c->rs.p, 0, S * 4, st));
@@ -700,6 +704,26 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
   cfg.stage_count = c->stage_count && (bound == 0 || bound > c->lane_max);
+  // deferred packed bodies when records above lane_max may be walked from HBM: one 64-row block
+  // (2,048 entries of 16 bytes) per 256 KiB of input, at least 16
+  o.dq = nullptr;
+  o.dq_cnt = nullptr;
+  o.dq_blocks = 0;
+  cfg.body_count = false;
+  if (n && (bound == 0 || bound > c->lane_max)) {
+    uint64_t blocks = nbytes >> 18;
+    blocks = blocks < 16 ? 16 : (blocks > (1u << 16) ? (1u << 16) : blocks);
+    const size_t qb = (size_t)blocks * 64u * kDeferK * 16u, cb = (size_t)blocks * 64u;
+    if ((c->dq.cap < qb || c->dq_cnt.cap < cb) && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    if (c->dq.ensure(qb) || c->dq_cnt.ensure(cb)) {
+      set_error("device allocation failed (deferred bodies)");
+      return TFRG_E_NOMEM;
+    }
+    o.dq = c->dq.as<uint4>();
+    o.dq_cnt = c->dq_cnt.as<uint8_t>();
+    o.dq_blocks = (uint32_t)blocks;
+    cfg.body_count = true;
+  }
   if (n) {
     hipEvent_t* ev = nullptr;
     if (c->profiling) {

@@ -99,8 +99,17 @@ enum InfoIdx : uint32_t {
   kInfoBytesTicket = 12, // k_bytes_scan tile tickets
   kInfoBytesBig = 13,    // k_bytes_scan: long elements listed for the wave copy
   kInfoCrcCtr = 14,      // [14..15] u64: streaming-CRC list entries << kCrcIdxShift | flat 1 KiB rounds
-  kInfoCount = 16
+  kInfoDefer = 16,       // k_lane_count: 64-record rows of deferred packed-int64 bodies reserved (k_body_count)
+  kInfoCount = 20
 };
+
+// Deferred packed int64 bodies of records walked from HBM (k_lane_count -> k_body_count): a wave
+// reserves one block of 64 rows, row = one record, kDeferK entries (record, slot, absolute body
+// offset, length) and a count byte per row
+constexpr uint32_t kDeferK = 32;
+// status of a record whose deferred body did not count canonically (k_body_count): k_tail_count's
+// exact walker withdraws its columns and re-walks it (never left in the status column)
+constexpr int32_t kStatusRedo = 0x7fff0001;
 
 // verdict byte of a record the lane kernel left to the exact walker (k_tail_count role 1 writes its
 // final verdict, payload CRC included); role 2 (payload CRCs of large records) skips such records,
@@ -147,6 +156,9 @@ struct DevOut {
   uint64_t* crc_part;    // [n] rounds done << 32 | XOR of the slices, of a record split over waves
   uint32_t* irr;         // [n_slots] records not placed speculatively per slot (DevSchema::spec; after
                          // the scan words in their buffer, zero between decodes: k_tail_gather clears)
+  uint4* dq;             // [dq_blocks][64][kDeferK] deferred bodies (nullptr: no deferral this decode)
+  uint8_t* dq_cnt;       // [dq_blocks][64] entries used per row (0 for records not accepted)
+  uint32_t dq_blocks;
 };
 
 // Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)
@@ -191,11 +203,12 @@ struct LaunchCfg {
   uint32_t lane_max;       // records above this size go to the wave kernels
   uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
   bool stage_count;        // the batch may hold staged records above lane_max: launch k_stage_count
+  bool body_count;         // deferred packed bodies possible (DevOut::dq): launch k_body_count
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageStageCount, kStageTailCount, kStageSpine, kStageDownGather,
-                   kStageTailGather, kStageMaterialize, kNumStages };
+enum Stage : int { kStageLaneCount = 0, kStageStageCount, kStageBodyCount, kStageTailCount, kStageSpine,
+                   kStageDownGather, kStageTailGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

@@ -1149,10 +1149,38 @@ __device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e,
 #ifndef TFRG_HBM_BLOCKS
 #define TFRG_HBM_BLOCKS 2
 #endif
+// bit 7 of the 16 bytes of a block, byte i -> bit i
+__device__ __forceinline__ uint32_t cont16(uint4 b) {
+  auto nib = [](uint32_t w) {
+    w = (w >> 7) & 0x01010101u;
+    return (w | (w >> 7) | (w >> 14) | (w >> 21)) & 0xfu;
+  };
+  return nib(b.x) | (nib(b.y) << 4) | (nib(b.z) << 8) | (nib(b.w) << 12);
+}
+// One 16-byte block of a packed chunk, bytes [lo, hi) of it inside the chunk: its terminators added,
+// the run of continuation bytes carried in / out, `bad` set by a varint of more than 10 bytes (runs
+// of >= 10 continuation bytes after a terminator found by a 10-fold AND of shifts)
+__device__ __forceinline__ void packed_block(uint4 blk, uint32_t lo, uint32_t hi, uint32_t& run, uint32_t& terms,
+                                             bool& bad) {
+  const uint32_t valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+  const uint32_t m = cont16(blk), t = ~m & valid, cm = m & valid;
+  const uint32_t a = cm & (cm >> 1), b = a & (a >> 2), c = b & (b >> 4);
+  bad |= ((c & (a >> 8)) & (t << 1)) != 0u;
+  if (!t) {
+    run += hi - lo;
+  } else {
+    bad |= run + (uint32_t)__builtin_ctz(t) - lo >= 10u;  // the run carried in, ended here
+    run = hi - 1u - (31u - (uint32_t)__builtin_clz(t));
+    terms += (uint32_t)__popc(t);
+  }
+  bad |= run >= 10u;
+}
 // count_packed over HBM (records walked from HBM): aligned 16-byte blocks, two loads in flight per
 // round instead of one dependent dword pair per word (a packed list of 300 bytes was 75 serial
 // round trips; four blocks per round would cost the staged path its occupancy in VGPRs)
-template <bool WIN>
+// (NB blocks per round: k_body_count, whose lanes count independent bodies, takes 8: one round for
+// a body of up to ~112 bytes)
+template <int NB = TFRG_HBM_BLOCKS, bool WIN>
 __device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o, uint32_t e, uint32_t& cnt) {
 #ifdef TFRG_DIAG_NOCOUNT  // diagnostic build (timing only, wrong counts): no loads of packed bodies
   cnt = (e - o) >> 2;
@@ -1160,32 +1188,48 @@ __device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o,
 #endif
   uint32_t run = 0, terms = 0;
   const uint64_t a0 = s.base + o, a1 = s.base + e;
-  const uint64_t lb = s.lim - 12;  // last readable 16-byte block
-  for (uint64_t q = a0 & ~15ull; q < a1; q += 16 * TFRG_HBM_BLOCKS) {
-    uint4 blk[TFRG_HBM_BLOCKS];
+  // last block to load: the chunk's last one (spare loads of a round re-read it: no line past the
+  // chunk is fetched), never past the last readable 16-byte block
+  const uint64_t lb0 = s.lim - 12, lbc = a1 > a0 ? (a1 - 1) & ~15ull : a0 & ~15ull;
+  const uint64_t lb = lbc < lb0 ? lbc : lb0;
+  for (uint64_t q = a0 & ~15ull; q < a1; q += 16 * NB) {
+    uint4 blk[NB];
 #pragma unroll
-    for (int j = 0; j < TFRG_HBM_BLOCKS; ++j) {
+    for (int j = 0; j < NB; ++j) {
       const uint64_t qq = q + 16u * j;
       blk[j] = *reinterpret_cast<const uint4*>(s.buf + (qq < lb ? qq : lb));
     }
+    if constexpr (NB > 2) {  // (k_body_count: a block at a time)
+      bool bad = false;
 #pragma unroll
-    for (int j = 0; j < TFRG_HBM_BLOCKS; ++j) {
-      const uint32_t ws[4] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w};
+      for (int j = 0; j < NB; ++j) {
+        const uint64_t qb = q + 16u * j;
+        if (qb >= a1) break;
+        const uint32_t lo = a0 > qb ? (uint32_t)(a0 - qb) : 0u;
+        const uint32_t hi = a1 - qb < 16u ? (uint32_t)(a1 - qb) : 16u;
+        packed_block(blk[j], lo, hi, run, terms, bad);
+      }
+      if (bad) return false;
+    } else {  // (the lane kernel's walk: a word at a time, fewer live registers)
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint64_t wa = q + 16u * j + 4u * k;
-        if (wa >= a1 || wa + 4 <= a0) continue;
-        const uint32_t lo = wa < a0 ? (uint32_t)(a0 - wa) : 0u;  // valid bytes [lo, hi) of this word
-        const uint32_t hi = wa + 4 <= a1 ? 4u : (uint32_t)(a1 - wa);
-        const uint32_t vm = bytes_mask(hi) & ~((1u << (lo << 3)) - 1u);
-        const uint32_t term = ~ws[k] & vm & 0x80808080u;
-        if (!term) {
-          run += hi - lo;
-          if (run >= 10) return false;
-        } else {
-          if (run + (__builtin_ctz(term) >> 3) - lo >= 10) return false;
-          run = hi - 1u - ((31u - __builtin_clz(term)) >> 3);
-          terms += __popc(term);
+      for (int j = 0; j < NB; ++j) {
+        const uint32_t ws[4] = {blk[j].x, blk[j].y, blk[j].z, blk[j].w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint64_t wa = q + 16u * j + 4u * k;
+          if (wa >= a1 || wa + 4 <= a0) continue;
+          const uint32_t lo = wa < a0 ? (uint32_t)(a0 - wa) : 0u;  // valid bytes [lo, hi) of this word
+          const uint32_t hi = wa + 4 <= a1 ? 4u : (uint32_t)(a1 - wa);
+          const uint32_t vm = bytes_mask(hi) & ~((1u << (lo << 3)) - 1u);
+          const uint32_t term = ~ws[k] & vm & 0x80808080u;
+          if (!term) {
+            run += hi - lo;
+            if (run >= 10) return false;
+          } else {
+            if (run + (__builtin_ctz(term) >> 3) - lo >= 10) return false;
+            run = hi - 1u - ((31u - __builtin_clz(term)) >> 3);
+            terms += __popc(term);
+          }
         }
       }
     }
@@ -1353,8 +1397,29 @@ __device__ __forceinline__ bool hdr2(const S& s, uint32_t pos, uint32_t end, uin
 // Returns TFRG_OK with the dict in sink.ord / cnt (or count) / loc, or kBail (exact walker).
 // Every level is a single canonical pass: one Features field spanning the Example, map entries of
 // exactly (key #1, value #2), one kind field spanning the Feature, list chunks of field #1.
-template <bool COMPAT, class Sink, class S>
-__device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sink) {
+// Deferred counting of packed int64 bodies (records walked from HBM). Counting a list's packed
+// chunk on the spot costs the lane a dependent HBM round trip per 32 bytes of every body, one list
+// after the other: 58 % of C3's count pass (0.72 -> 0.30 ms in a build that skipped those loads).
+// Instead the lane lists (record, slot, absolute body offset, length) in its record's row and leaves
+// the count word 0; k_body_count then counts every listed body in one flat pass, all of them
+// independent (bandwidth, not latency), and writes the count words and tile sums. A body that does
+// not count canonically sends its record to the exact walker, which withdraws its columns first.
+struct NoDefer {
+  __device__ __forceinline__ bool push(uint32_t, uint64_t, uint32_t) const { return false; }
+};
+struct BodyDefer {
+  uint4* row;  // entry 0 of this lane's record (nullptr: count on the spot); entry j at row[64 j]
+  uint32_t r;
+  mutable uint32_t n = 0;
+  __device__ __forceinline__ bool push(uint32_t slot, uint64_t at, uint32_t len) const {
+    if (!row || n >= kDeferK) return false;
+    row[64u * n++] = make_uint4(r, slot, (uint32_t)at, len);  // (a batch is < 4 GiB)
+    return true;
+  }
+};
+
+template <bool COMPAT, class Sink, class S, class D = NoDefer>
+__device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sink, const D& dfr = D{}) {
   const uint32_t L = s.L;
   uint32_t fn, fo, fl;
   bool ok = hdr2(s, 0, L, fn, fo, fl) & (fn == 1u) & (fo + fl == L);
@@ -1393,9 +1458,13 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
         cnt += __popc(tm);
         if (nch == 0) c0w = w;
       } else {
-        uint32_t k = 0;
-        ok &= count_packed(s, co, co + cl, k);
-        cnt += k;
+        // the list's only chunk, of a known key: its count can wait for k_body_count
+        const int dslot = (nch == 0 && g == le && kid >= 0) ? (int)K.rec[(uint32_t)kid * kKrWords + kKrSlot1 + 2u] : -1;
+        if (!(dslot >= 0 && dfr.push((uint32_t)dslot, s.base + co, cl))) {
+          uint32_t k = 0;
+          ok &= count_packed(s, co, co + cl, k);
+          cnt += k;
+        }
       }
       if (nch == 0) {
         c0o = co;
@@ -1959,6 +2028,14 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
     // computed here, serially per lane from HBM.
     const bool bigw = fast_ok && valid && ((!mine && !stg) || (span_rec && !staged));
     if (__ballot(bigw)) {
+      // one block of deferred-body rows per wave (k_body_count), while the batch has room
+      uint32_t blk = ~0u;
+      if (MODE != 0 && o.dq) {  // (MODE 0, narrow schemas: its register budget keeps the in-place count)
+        if (lane == 0) blk = atomicAdd(&o.info[kInfoDefer], 1u);
+        blk = rfl32((uint32_t)__shfl((int)blk, 0, 64));
+        if (blk >= o.dq_blocks) blk = ~0u;
+      }
+      uint32_t nd = 0;
       if (bigw) {
         // (the payload CRC of a large record is role 2's stream, unless it is shorter than one round)
         const bool crc_here = mine || (uint64_t)v.L < kCrcListMin;
@@ -1966,10 +2043,17 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
         sink.fast_reset(S);
         if (strict_pass(B, v.verdict, crc_here)) {
           const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
-          done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+          if constexpr (MODE != 0) {
+            const BodyDefer dfr{blk != ~0u ? o.dq + (size_t)blk * 64u * kDeferK + lane : nullptr, r};
+            done = fast_walk<COMPAT>(fg, K, sink, dfr) == TFRG_OK;
+            nd = dfr.n;
+          } else {
+            done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+          }
           tried = true;
         }
       }
+      if (MODE != 0 && blk != ~0u) o.dq_cnt[(size_t)blk * 64u + lane] = (uint8_t)(bigw && done ? nd : 0u);
     }
     PHASE_MARK(p4);
     // everything else of this wave's records goes to the exact walker
@@ -2039,6 +2123,77 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
   }
 }
 
+// The columns a record accepted by the lane kernel wrote, withdrawn before the exact walker redoes it:
+// order / count of every slot cleared, the counts taken back from the tile sums, and every present
+// slot counted irregular (a speculatively placed value of the record is then re-placed by the scan).
+__device__ void withdraw_record(const DevOut& o, uint32_t n, uint32_t n_slots, uint32_t r) {
+  for (uint32_t k = 0; k < n_slots; ++k) {
+    const size_t at = (size_t)k * n + r;
+    const uint32_t c = o.count[at];
+    if (o.order[at]) o.order[at] = 0;
+    if (!c) continue;
+    o.count[at] = 0;
+    atomicAdd(&o.irr[k], 1u);
+    if (c & ~kCountInline) atomicSub(&o.tsum[(size_t)k * o.tile_stride + (r >> kTileShift)], c & ~kCountInline);
+  }
+}
+
+// Counts of the deferred packed int64 bodies (BodyDefer). A block holds the rows of one lane-kernel
+// wave: 64 consecutive records (one tile), entry j of every row side by side ([block][j][lane]). A
+// wave takes a quarter of a block's entry columns, lane l its record's entries one after the other:
+// the lanes of one step are 64 records' j-th bodies, usually one slot of one tile, so the tile sum is
+// usually one atomic per step. Each body: count_packed over HBM with 8 blocks of 16 bytes in flight
+// (one round for most bodies), the count word written. A body that does not count canonically (a
+// varint of more than 10 bytes, or one running past the chunk) marks its record kStatusRedo (once)
+// and lists it for the exact walker (k_tail_count role 1), which withdraws the record's columns and
+// re-walks it.
+constexpr int kBodyBlock = 256;
+constexpr uint32_t kBodyParts = 4;  // waves per block of rows (kDeferK / kBodyParts columns each)
+__global__ __launch_bounds__(kBodyBlock) void k_body_count(DevBatch B, DevOut o) {
+  const uint32_t nblk = o.info[kInfoDefer] < o.dq_blocks ? o.info[kInfoDefer] : o.dq_blocks;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t lim = ((B.nbytes + 15) & ~15ull) - 4;
+  const uint32_t nw = gridDim.x * (kBodyBlock / 64u);
+  for (uint32_t t = blockIdx.x * (kBodyBlock / 64u) + rfl32(threadIdx.x >> 6); t < nblk * kBodyParts; t += nw) {
+    const uint32_t blk = t / kBodyParts, j0 = (t % kBodyParts) * (kDeferK / kBodyParts);
+    const uint32_t nrow = o.dq_cnt[(size_t)blk * 64u + lane];
+    uint32_t jmax = nrow;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const uint32_t y = (uint32_t)__shfl_xor((int)jmax, m, 64);
+      jmax = y > jmax ? y : jmax;
+    }
+    jmax = rfl32(jmax);
+    const uint32_t j1 = j0 + kDeferK / kBodyParts < jmax ? j0 + kDeferK / kBodyParts : jmax;
+    for (uint32_t j = j0; j < j1; ++j) {  // (wave-uniform: the reductions below see every lane)
+      bool has = j < nrow, ok = true;
+      uint32_t r = 0, slot = 0, cnt = 0;
+      if (has) {
+        const uint4 q = o.dq[((size_t)blk * kDeferK + j) * 64u + lane];
+        r = q.x;
+        slot = q.y;
+        const FastSrcG<false> s{B.bytes, (uint64_t)q.z, q.w, lim};
+        ok = count_packed<8>(s, 0u, q.w, cnt);
+      }
+      if (has && ok) o.count[(size_t)slot * B.n + r] = cnt;
+      if (has && !ok && atomicCAS(&o.status[r], TFRG_OK, kStatusRedo) == TFRG_OK) {
+        const uint32_t si = atomicAdd(&o.info[kInfoSlow], 1u);
+        o.slow_list[si] = r;
+      }
+      // tile sums: one atomic per run of lanes with the same slot (the rows share one tile)
+      bool pend = has && ok && cnt != 0u;
+      for (uint64_t m = __ballot(pend); m; m = __ballot(pend)) {
+        const int l0 = __builtin_ctzll(m);
+        const uint32_t s0 = (uint32_t)__shfl((int)slot, l0, 64), t0 = (uint32_t)__shfl((int)r, l0, 64) >> kTileShift;
+        const bool mine = pend && slot == s0 && (r >> kTileShift) == t0;
+        const uint32_t sum = wave_sum_u32(mine ? cnt : 0u);
+        if (lane == (uint32_t)l0) atomicAdd(&o.tsum[(size_t)s0 * o.tile_stride + t0], sum);
+        pend &= !mine;
+      }
+    }
+  }
+}
+
 // Exact reference walk (decoder.pyx:107-300 in its own level-by-level error precedence), one lane per
 // record of the slow list, reading the record from HBM; also the framing errors and schema misses.
 template <int R, bool COMPAT, bool GORD, uint32_t BLK>
@@ -2056,6 +2211,7 @@ __device__ void role_slow_count(const DevBatch& B, const DevSchema& sc, const De
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
   for (uint32_t i = blockIdx.x * BLK + threadIdx.x; i < nslow; i += gridDim.x * BLK) {
     const uint32_t r = o.slow_list[i];
+    if (o.status[r] == kStatusRedo) withdraw_record(o, B.n, S, r);  // (a body k_body_count rejected)
     RecView v = rec_view(B, r);
     int64_t aux = 0;
     CountSinkT<!GORD> sink{&sc, &o, dict_ord<!GORD>(o.order + r, ord + threadIdx.x),
@@ -2814,14 +2970,6 @@ __device__ __forceinline__ bool sg_payload_crc(const uint8_t* l, uint32_t a, uin
   return v == S;
 }
 
-// bit 7 of the 16 bytes of a block, byte i -> bit i
-__device__ __forceinline__ uint32_t cont16(uint4 b) {
-  auto nib = [](uint32_t w) {
-    w = (w >> 7) & 0x01010101u;
-    return (w | (w >> 7) | (w >> 14) | (w >> 21)) & 0xfu;
-  };
-  return nib(b.x) | (nib(b.y) << 4) | (nib(b.z) << 8) | (nib(b.w) << 12);
-}
 
 // count_packed over the LDS stage, one aligned 16-byte block per step (one ds_read_b128) and the
 // block's 16 continuation bits at once: terminators = popcount, the run of continuation bytes
@@ -2835,18 +2983,7 @@ __device__ __forceinline__ bool count_packed16(const FastSrc& s, uint32_t o, uin
   for (uint32_t q = a0 & ~15u; q < a1; q += 16u) {
     const uint4 blk = *reinterpret_cast<const uint4*>(s.l + q);
     const uint32_t lo = a0 > q ? a0 - q : 0u, hi = a1 - q < 16u ? a1 - q : 16u;  // valid bytes [lo, hi)
-    const uint32_t valid = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-    const uint32_t m = cont16(blk), t = ~m & valid, cm = m & valid;
-    const uint32_t a = cm & (cm >> 1), b = a & (a >> 2), c = b & (b >> 4);
-    bad |= ((c & (a >> 8)) & (t << 1)) != 0u;  // >= 10 continuation bytes right after a terminator
-    if (!t) {
-      run += hi - lo;
-    } else {
-      bad |= run + (uint32_t)__builtin_ctz(t) - lo >= 10u;  // the run carried in, ended here
-      run = hi - 1u - (31u - (uint32_t)__builtin_clz(t));
-      terms += (uint32_t)__popc(t);
-    }
-    bad |= run >= 10u;
+    packed_block(blk, lo, hi, run, terms, bad);
   }
   if (bad || (e > o && run)) return false;  // the last varint runs past the chunk
   cnt = terms;
@@ -4076,7 +4213,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 #endif
 constexpr size_t kLaneLdsBudget = TFRG_LANE_LDS_BUDGET;  // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_stage_count", "k_tail_count", "k_spine",
+const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_stage_count", "k_body_count", "k_tail_count", "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -4139,6 +4276,11 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       per_cu = 1;
     const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
     hipLaunchKernelGGL((k_stage_count<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, d_tab, d_consts);
+  }
+  mark(kStageBodyCount);
+  if (cfg.body_count) {  // the deferred packed bodies of the records walked from HBM
+    const uint32_t g = 8u * (uint32_t)cfg.num_cus;
+    hipLaunchKernelGGL(k_body_count, dim3(g), dim3(kBodyBlock), 0, st, b, o);
   }
   mark(kStageTailCount);
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
