@@ -4278,7 +4278,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     hipLaunchKernelGGL((k_stage_count<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, d_tab, d_consts);
   }
   mark(kStageBodyCount);
-  if (cfg.body_count) {  // the deferred packed bodies of the records walked from HBM
+  if (cfg.body_count && lane_lds > kLaneLdsBudget) {  // deferred bodies (lane modes 1 and 2 only)
     const uint32_t g = 8u * (uint32_t)cfg.num_cus;
     hipLaunchKernelGGL(k_body_count, dim3(g), dim3(kBodyBlock), 0, st, b, o);
   }
