@@ -110,3 +110,33 @@ def test_listing_bound_payloads():
         _check(d, b, st, en)
     finally:
         d.close()
+
+
+@pytest.mark.parametrize("strict", [False, True])
+def test_stage_size_payloads(strict):
+    """Payloads of ~12 KiB (the wavefront kernels' stage size) at every alignment through the flat
+    streaming CRC, every third corrupted near its start, middle or end. Strict mode: a corrupted
+    record is DataLossError (status 15) and the others decode. (A wave-per-record CRC for payloads
+    up to 12,288 bytes, lane l a 192-byte slice, passed this test and was slower: C3 CRC 0.40 ->
+    0.57 ms.)"""
+    pl = []
+    for k, n in enumerate(range(12150, 12330, 7)):  # blob length -> payloads around the bound
+        pl.append(_bytes_record(n, 900 + k))
+    buf, st, en = synth.framed(pl)
+    b = buf.copy()
+    bad = set()
+    for i in range(0, len(st), 3):
+        lp = int(en[i]) - int(st[i]) - 16
+        b[int(st[i]) + 12 + (12, lp // 2, lp - 16)[i % 3]] ^= 0x20  # (inside the blob: still decodes)
+        bad.add(i)
+    d = hip.HipDecoder(0)
+    try:
+        d.set_lane_max(0)
+        if strict:
+            res = d.decode(b, st, en, strict_crc=True)
+            for i in range(len(st)):
+                assert int(res.status[i]) == (15 if i in bad else 0), i
+        else:
+            _check(d, b, st, en)
+    finally:
+        d.close()
