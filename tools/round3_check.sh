@@ -22,7 +22,7 @@ for k, v in d.get("configs", {}).items():
 PY
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu > $O/prof.log 2>&1 \
   || { echo "rocprof failed"; tail -20 $O/prof.log; exit 1; }
-for bb in 2147483648 4026531840; do
+for bb in 2147483648; do  # (3.75 GiB batches: ~13x their size in value arenas per context, see DESIGN)
   timeout -k 10 200 python bench.py --only c4 --no-cpu --batch-bytes $bb > $O/bb_$bb.json 2> $O/bb_$bb.err || { tail $O/bb_$bb.err; exit 1; }
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('batch', sys.argv[2], d['value'], d['ms_per_step'], d['config']['batches_per_gpu'])" $O/bb_$bb.json $bb
 done
