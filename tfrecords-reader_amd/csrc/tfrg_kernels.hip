@@ -3548,7 +3548,10 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
                                                             uint32_t n_tiles) {
   // slots per scan group (one barrier each): 2 beside 4 tiles per workgroup, 8 with one tile (small
   // batches and wide schemas: fewer barriers between the loads, same registers)
-  constexpr uint32_t kDG = kDT == 1 ? 8u : 2u;
+#ifndef TFRG_DG1
+#define TFRG_DG1 8
+#endif
+  constexpr uint32_t kDG = kDT == 1 ? (uint32_t)TFRG_DG1 : 2u;
   __shared__ uint32_t s_w[2][kDT * kDG][4];  // wave totals, double-buffered across slot groups
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t S = sc.n_slots;
@@ -4032,7 +4035,11 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
   constexpr int kFG = 8;
+#ifdef TFRG_DIAG_NOFLOAT  // diagnostic build (timing only, values missing): no float copies
+  uint64_t m = 0;
+#else
   uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
+#endif
   while (m) {
     uint32_t fb[kFG], fn[kFG];
     uint64_t fd[kFG];
@@ -4063,8 +4070,12 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
 #ifndef TFRG_INT64_RING
 #define TFRG_INT64_RING 1
 #endif
+#ifdef TFRG_DIAG_NOINT64  // diagnostic build (timing only, values missing): no int64 decode
+  int rr = 1;
+#else
   int rr = TFRG_INT64_RING ? int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring) : -1;
   if (rr < 0) rr = int64_balanced<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane) ? 1 : 0;
+#endif
   if (!rr) fail |= iv;
   PHASE_MARK(g1);
   PHASE_ADD(11, gf, g1);
