@@ -403,17 +403,27 @@ __device__ __forceinline__ void spec_target(uint32_t* dst, const DevOut& o, uint
 }
 
 // put_inline at a staged target (record r of the batch)
+// Column stores of the lane kernel: written once, never re-read by it (TFRG_NT_STORES = 1: with the
+// nontemporal hint, a measured-only build option)
+#ifndef TFRG_NT_STORES
+#define TFRG_NT_STORES 0
+#endif
+template <class T>
+__device__ __forceinline__ void st_col(T* p, T v) {
+  if constexpr (TFRG_NT_STORES) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
 __device__ __forceinline__ void put_spec(const lds_spec_t* t, uint2 lc, uint32_t r) {
   const spec_u32x4 a = t[0], b = t[1];
   if (r >= b.x) return;
   const uint64_t p1 = ((uint64_t)a.y << 32) | a.x;
   if (b.y == TFRG_KIND_INT64) {
-    reinterpret_cast<uint2*>(p1)[r] = lc;
+    st_col(reinterpret_cast<uint64_t*>(p1) + r, ((uint64_t)lc.y << 32) | lc.x);
   } else if (b.y == TFRG_KIND_FLOAT) {
-    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
+    st_col(reinterpret_cast<uint32_t*>(p1) + r, lc.x);
   } else {
-    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
-    reinterpret_cast<uint32_t*>(((uint64_t)a.w << 32) | a.z)[r] = lc.y;
+    st_col(reinterpret_cast<uint32_t*>(p1) + r, lc.x);
+    st_col(reinterpret_cast<uint32_t*>(((uint64_t)a.w << 32) | a.z) + r, lc.y);
   }
 }
 
@@ -2069,8 +2079,8 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
       }
     }
     if (done) {
-      o.status[r] = TFRG_OK;
-      o.verdict[r] = (uint8_t)v.verdict;
+      st_col(o.status + r, (int32_t)TFRG_OK);
+      st_col(o.verdict + r, (uint8_t)v.verdict);
     }
     // the payload CRC of an accepted large record: one entry of the streaming CRC list
     const bool crc_on = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
@@ -2096,11 +2106,11 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
       const uint32_t c = ov ? sink.count_of(k) : 0u;
       if (done) {
         const size_t at = (size_t)k * B.n + r;
-        o.order[at] = (uint16_t)ov;
+        st_col(o.order + at, (uint16_t)ov);
 #ifdef TFRG_DIAG_NOCNT  // diagnostic build: no count word for regular speculatively placed values
         if (!(spec_on && spec_l[k] && mine && c == (1u | kCountInline)))
 #endif
-        o.count[at] = c;
+        st_col(o.count + at, c);
       }
       const uint32_t x = c & ~kCountInline;
       const uint64_t nz = __ballot(x != 0u);
@@ -2109,7 +2119,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
         if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
       }
       if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
-        if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
+        if (valid) st_col(o.rs + (size_t)k * (B.n + 1) + r, r);
         const uint64_t irm = __ballot(valid && !stg && !(done && c == (1u | kCountInline)));
         if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
       }
