@@ -8,7 +8,7 @@ uniform in +-50 % around 2^19 (~29 MiB per file, 7.36 GiB / 134 M records in all
 partitioned over the N ranks by LPT on bytes (tfr_reader/shard.py): strong scaling, N = 1 decodes
 all 256 files, N = 8 about 32 per GPU; no collective on the data path. Each rank indexes its files
 with the native framing indexer, keeps its whole shard resident in HBM and decodes it as record-range
-batches of <= 1 GiB (tfr_reader.shard.ShardDecoder: one context per batch, batches spread over two
+batches of <= 2 GiB (tfr_reader.shard.ShardDecoder: one context per batch, batches spread over two
 streams). A step is one full decode of the shard (framing check + masked CRC-32C of length and
 payload + reference-exact Example decode + columnar gather of every value), inputs already in HBM.
 
@@ -52,7 +52,10 @@ def parse_args(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--files", type=int, default=N_FILES, help="files in the C4 directory (partitioned over ranks)")
-    ap.add_argument("--batch-bytes", type=int, default=1 << 30, help="bytes per decode call of a rank's shard")
+    # 2 GiB batches: 2,170 -> 2,229 GiB/s over 1 GiB on one box, +0.9 / +2.3 % on two others
+    # (profiles/r03/sweep, profiles/r03/bench_c4_batch2GiB*.json); the value arenas scale with the
+    # batch, so the total device memory of a shard is the same
+    ap.add_argument("--batch-bytes", type=int, default=1 << 31, help="bytes per decode call of a rank's shard")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the shard's batches are spread over")
     ap.add_argument("--only", default=None, choices=["c4", "c1file", "c2", "c3", "c4c2", "c4of8"],
                     help="measure one config only and report it as the headline (profiling runs)")
