@@ -2158,7 +2158,10 @@ __device__ void withdraw_record(const DevOut& o, uint32_t n, uint32_t n_slots, u
 // and lists it for the exact walker (k_tail_count role 1), which withdraws the record's columns and
 // re-walks it.
 constexpr int kBodyBlock = 256;
-constexpr uint32_t kBodyParts = 4;  // waves per block of rows (kDeferK / kBodyParts columns each)
+#ifndef TFRG_BODY_PARTS
+#define TFRG_BODY_PARTS 4
+#endif
+constexpr uint32_t kBodyParts = TFRG_BODY_PARTS;  // waves per block of rows (kDeferK / kBodyParts columns each)
 __global__ __launch_bounds__(kBodyBlock) void k_body_count(DevBatch B, DevOut o) {
   const uint32_t nblk = o.info[kInfoDefer] < o.dq_blocks ? o.info[kInfoDefer] : o.dq_blocks;
   const uint32_t lane = threadIdx.x & 63u;
@@ -4044,7 +4047,10 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
-  constexpr int kFG = 8;
+#ifndef TFRG_FG
+#define TFRG_FG 8
+#endif
+  constexpr int kFG = TFRG_FG;
 #ifdef TFRG_DIAG_NOFLOAT  // diagnostic build (timing only, values missing): no float copies
   uint64_t m = 0;
 #else
