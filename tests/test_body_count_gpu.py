@@ -84,3 +84,27 @@ def test_c3_deferred_matches_stage_count():
     assert a.info.n_big == len(pl)
     for name in ("status", "verdict", "order", "row_splits", "slot_base", "i64", "f32"):
         assert np.array_equal(getattr(a, name), getattr(b, name)), name
+
+
+def test_deferred_bodies_global_dict_mode():
+    """More than 64 slots (the lane kernel's global-column dict, MODE 2) with every record walked
+    from HBM: deferred bodies, bit-exact vs the oracle."""
+    rng = np.random.default_rng(11)
+    pl = []
+    for i in range(400):
+        ents = []
+        for j in range(70):
+            m = int(rng.integers(0, 12))
+            ents.append(entry(f"w{j}".encode(), i64(*[int(x) for x in rng.integers(-(2**35), 2**35, m)])))
+        pl.append(example(*ents))
+    buf, st, en = synth.framed(pl)
+    orc = O.Oracle()
+    d = hip.HipDecoder(0)
+    try:
+        d.set_lane_max(0)
+        r = d.decode(buf, st, en)
+        assert r.info.n_big == len(pl) and len(r.slot_key) >= 70
+        bad = _compare_to_oracle(r, orc, buf, st, en)
+    finally:
+        d.close()
+    assert not bad, bad[:10]
