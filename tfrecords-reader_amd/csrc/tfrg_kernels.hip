@@ -1525,6 +1525,9 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
 #ifndef TFRG_TPL_SMEM
 #define TFRG_TPL_SMEM 0
 #endif
+#ifndef TFRG_TPL_SPLIT
+#define TFRG_TPL_SPLIT 1  // template match and template CRC as two loops (0: one fused loop)
+#endif
 // One template's words. Control words (lengths, entry fields, CRC constants) are wave-uniform:
 // u() returns them in SGPRs, so the loops and mode tests over them are scalar branches; d() reads
 // the per-word bytes / mask as VALU operands. TFRG_TPL_SMEM = 1 reads them with scalar loads from
@@ -1575,6 +1578,39 @@ __device__ __forceinline__ TplHit tpl_match_u(const FastSrc& fs, bool cand0, Tpl
       const bool pc = crc && v0 != 0xffffffffu;
       const uint32_t w0 = pc ? v0 >> 2 : nw;
       uint32_t diff = 0, c = 0, prev = SW[0];
+#if TFRG_TPL_SPLIT
+      // the match over every word (no per-word CRC tests: scalar work is half the kernel's issue),
+      // then the CRC of the variable words in a counted loop of its own (they are read again)
+      for (uint32_t w = 0; w < nw; w += 4u) {
+        uint32_t x[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t next = SW[w + 1u + i];
+          x[i] = __builtin_amdgcn_alignbyte(next, prev, sh);
+          prev = next;
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) diff |= (x[i] ^ Tp.d(kTplBytes + w + i)) & Tp.d(kTplMask + w + i);
+      }
+      if (pc) {
+        const uint32_t nfull = Lu >> 2, rem = Lu & 3u;
+        uint32_t pv = SW[w0];
+        for (uint32_t wi = w0; wi < nfull; ++wi) {
+          const uint32_t next = SW[wi + 1u];
+          const uint32_t x = __builtin_amdgcn_alignbyte(next, pv, sh);
+          pv = next;
+          c = T.step4(c ^ (x & ~Tp.d(kTplMask + wi)));
+        }
+        if (rem) {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
+          const uint32_t x = __builtin_amdgcn_alignbyte(SW[nfull + 1u], pv, sh);
+          const uint32_t y = c ^ (x & ~Tp.d(kTplMask + nfull) & bytes_mask(rem));
+          uint32_t u = T(rem - 1u, y & 0xffu);
+          if (rem >= 2u) u ^= T(rem - 2u, (y >> 8) & 0xffu);
+          if (rem == 3u) u ^= T(0u, (y >> 16) & 0xffu);
+          c = u ^ (c >> (8u * rem));
+        }
+      }
+#else
       // four words per step: template words beyond L are zero (mask 0), the stage has 64 bytes of
       // slack past any record
       for (uint32_t w = 0; w < nw; w += 4u) {
@@ -1604,6 +1640,7 @@ __device__ __forceinline__ TplHit tpl_match_u(const FastSrc& fs, bool cand0, Tpl
           }
         }
       }
+#endif
       if (!diff) {
         h.t = (int)t;
         h.pc = pc;
