@@ -318,16 +318,16 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     vals = 8 * kt[3] + 4 * kt[2] + 8 * kt[1]
     present_small = int(present * n_small / max(n, 1))
     n_tiles = sum((int(r1 - r0) + 255) // 256 for r0, r1, _, _ in plan.tolist())
+    lane_alg = small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small
     alg = {
-        # lane kernel: its records' framed bytes + offsets in; status, verdict, order + count per slot
-        # and a location / single-value word per present list out
-        "k_lane_count": small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small,
+        # template path: its records' framed bytes + offsets in; status, verdict, order + row split
+        # (or count) per slot and a value / location word per present list out
+        "k_tpl_lane": lane_alg,
+        # lane kernel (all lane records when no template applies): the same compulsory bytes
+        "k_lane_count": lane_alg,
         # streaming payload CRC of the records above lane_max (their bytes + list entry and offsets);
         # the exact walker's slow list is empty on these workloads
         "k_tail_count": big_bytes + 32 * n_big,
-        # staged large records (<= 12 KiB): their framed bytes + offsets in; status, verdict and the
-        # order / count / loc words of every slot out
-        "k_stage_count": big_bytes + n_big * (16 + 5 + 14 * n_slots),
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         # out-of-line lists: every value written once (their record bytes are counted by the lanes)
@@ -505,10 +505,11 @@ def run(args) -> None:
             del m["_d_bytes"], m["_elapsed"]
             if name == "c4of8":  # the same share without record-shape templates (canonical walk only)
                 t = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps, templates=False)
+                lane_on = m["kernels_ms"].get("k_tpl_lane", 0.0) + m["kernels_ms"].get("k_lane_count", 0.0)
                 templates_off = {"workload": "c4of8", "ms_per_step": t["ms_per_step"], "GiB_s": t["GiB_s"],
                                  "k_lane_count_ms": t["kernels_ms"].get("k_lane_count"),
                                  "templates_on_ms_per_step": m["ms_per_step"],
-                                 "templates_on_k_lane_count_ms": m["kernels_ms"].get("k_lane_count")}
+                                 "templates_on_lane_kernels_ms": round(lane_on, 4)}
                 del t
             if hasattr(cw, "files_mine"):
                 m["files"] = cw.files_mine

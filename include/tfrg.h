@@ -108,11 +108,6 @@ int tfrg_ctx_create(int device, tfrg_ctx** out);
 int tfrg_ctx_destroy(tfrg_ctx* ctx);
 /* records larger than lane_max bytes take the wavefront-per-record kernels (default 2048) */
 int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
-/* Records above lane_max whose span fits the 12 KiB stage counted one wavefront per record from LDS
- * (k_stage_count: entry-parallel canonical walk + lane-parallel payload CRC) instead of one lane
- * per record from HBM plus the streaming CRC. Off by default (env TFRG_STAGE_COUNT=1): identical
- * results, measured slower on the wide-schema config so far. */
-int tfrg_ctx_set_stage_count(tfrg_ctx* ctx, int on);
 /* An upper bound on (end - start) of the records of the following tfrg_decode_device calls (0 =
  * unknown, the default). With a bound <= lane_max the batch has no large records and their count
  * kernel is not launched (a few microseconds per decode); a wrong bound still decodes correctly
@@ -123,15 +118,27 @@ int tfrg_ctx_set_record_bound(tfrg_ctx* ctx, uint64_t max_record_bytes);
 int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
 
 /* Record-shape templates (no reference counterpart: a fast path under decoder.pyx:107-300). Up to 4
- * shapes of canonical records (payload <= 256 bytes) -- every byte fixed except list contents, incl.
- * the continuation bits of packed int64 lists -- are learned from up to 4,096 host records; a record
- * equal to a template under its mask gets the template's dict without the canonical walk (its
- * values are still read from the record). Learned automatically from the first tfrg_decode_host
+ * shapes of canonical records (payload <= 240 bytes) -- every byte fixed except list contents, incl.
+ * the continuation bits of packed int64 lists -- are learned from up to 4,096 host records; a framed
+ * record equal to a template under its mask, with matching length field and CRCs, gets the
+ * template's dict without a walk (its values are still read from the record; k_tpl_lane, schemas of
+ * <= 16 slots, CRC verdicts on). Learned automatically from the first tfrg_decode_host
  * batch after each tfrg_set_schema; device-only callers pass a host sample here. Returns the number
  * of templates (0..4). tfrg_ctx_set_templates(ctx, 0) disables them (env TFRG_TEMPLATES=0). */
 int tfrg_learn_templates(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                          const uint64_t* h_end, uint32_t n, uint32_t flags);
 int tfrg_template_count(tfrg_ctx* ctx);
+/* The learned templates in their window form (u32 words, layout in csrc/tfrg_internal.h): up to cap
+ * words into out, the window size W (words) into *window_words; returns the template count. For
+ * checking a template against records on the host. */
+int tfrg_template_words(tfrg_ctx* ctx, uint32_t* out, uint64_t cap, uint32_t* window_words);
+/* Host only (no device): the templates tfrg_learn_templates would learn for the given key table
+ * (as tfrg_set_schema) from the given records, in window form into out; returns their count. */
+int tfrg_learn_templates_host(uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
+                              const uint32_t* key_flags, uint32_t n_slots, const uint32_t* slot_key,
+                              const uint8_t* slot_kind, const uint8_t* h_bytes, uint64_t nbytes,
+                              const uint64_t* h_start, const uint64_t* h_end, uint32_t n, uint32_t flags,
+                              uint32_t* out, uint64_t cap, uint32_t* window_words);
 int tfrg_ctx_set_templates(tfrg_ctx* ctx, int on);
 
 /* Per-kernel timing: with profiling on, every decode records HIP events on its stream around
@@ -148,6 +155,34 @@ int tfrg_profile_last(tfrg_ctx* ctx, float* ms, const char** names, int cap);
 int tfrg_set_schema(tfrg_ctx* ctx, uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
                     const uint32_t* key_flags, uint32_t n_slots, const uint32_t* slot_key,
                     const uint8_t* slot_kind);
+
+/* ---------------------------------------------------------------------------------------------
+ * Host decode of ONE payload (replaces cython/decoder.pyx:107 example_from_bytes for single
+ * records: the "cython" decoder type, and the one-record calls decode(raw) / example_from_bytes /
+ * ds[i] of the "hip" type, far below the device's launch latency). The reference's exact
+ * semantics (error precedence, dict rules, varint compat mode unless TFRG_FLAG_SPEC_VARINT) on the
+ * calling thread; no device, no schema. One context per host thread.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct tfrg_host_ctx tfrg_host_ctx;
+typedef struct tfrg_host_record {
+  int32_t status;            /* tfrg_status of the record (0 = ok), as the device's status column */
+  uint32_t n_entries;        /* dict entries (status 0), in the reference's dict order */
+  int64_t aux;               /* error detail, as the device's aux column */
+  const uint32_t* key_off;   /* entry e's key: payload bytes [key_off[e], key_off[e] + key_len[e]) */
+  const uint32_t* key_len;
+  const uint8_t* kind;       /* tfrg_kind of entry e */
+  const uint32_t* val_off;   /* entry e's values: [val_off[e], val_off[e] + val_cnt[e]) of its kind's array */
+  const uint32_t* val_cnt;
+  const int64_t* i64;
+  const uint32_t* f32;       /* raw bits */
+  const uint32_t* b_off;     /* bytes elements: payload-relative (offset, length) */
+  const uint32_t* b_len;
+} tfrg_host_record;
+int tfrg_host_ctx_create(tfrg_host_ctx** out);
+int tfrg_host_ctx_destroy(tfrg_host_ctx* ctx);
+/* Decodes payload[0, len) into *out (arrays owned by ctx, valid until its next call). Returns 0 or a
+ * TFRG_E_* code; data errors are out->status. */
+int tfrg_host_decode(tfrg_host_ctx* ctx, const uint8_t* payload, uint64_t len, uint32_t flags, tfrg_host_record* out);
 
 /* Asynchronous decode of n records [start[i], end[i]) of a device buffer (framed TFRecords unless
  * TFRG_FLAG_PAYLOAD_ONLY). d_bytes must stay readable up to round_up(nbytes, 16) and nbytes must be
@@ -171,6 +206,8 @@ typedef struct tfrg_info {
   uint64_t kind_totals[4];  /* values per kind: [1] bytes elements, [2] floats, [3] int64s */
   uint64_t nbytes;
   uint64_t bytes_data_len;  /* TFRG_FLAG_MATERIALIZE_BYTES: bytes in the byte column, else 0   */
+  uint32_t tpl_groups_missed; /* 64-record groups with a record no record-shape template took */
+  uint32_t reserved;
 } tfrg_info;
 
 /* Waits for the last decode and returns its summary. */

@@ -68,16 +68,17 @@ def test_deferred_bodies_vs_oracle(seed):
     assert any(int(s) != 0 for s in r.status)  # the 11-byte varints are reported as errors
 
 
-def test_c3_deferred_matches_stage_count():
-    """C3-shaped batch through the deferred HBM walk and through k_stage_count (one wavefront per
-    staged record, its own packed counting from LDS): identical columns."""
+def test_c3_deferred_vs_oracle():
+    """C3-shaped batch, every record walked from HBM (lane_max 0) with its packed bodies deferred:
+    bit-exact vs the oracle, and identical to the default lane_max's decode."""
     pl = synth.c3_payloads(600, seed=3)
     buf, st, en = synth.framed(pl)
     d = hip.HipDecoder(0)
     try:
         d.set_lane_max(0)
         a = d.decode(buf, st, en)
-        d.set_stage_count(True)
+        assert not _compare_to_oracle(a, O.Oracle(), buf, st, en)
+        d.set_lane_max(hip.DEFAULT_LANE_MAX)
         b = d.decode(buf, st, en)
     finally:
         d.close()

@@ -63,3 +63,15 @@ def test_feature_surface(batch):
     assert f != r.feature(1)
     last = r.feature(len(r) - 1)
     assert last["e"].value == [b"", b"x"] and last["z"].value == []
+
+
+def test_features_pickle_as_plain_features(batch):
+    """A device-path Feature pickles as a plain Feature of its values (no batch reference)."""
+    import pickle
+
+    _, _, _, r = batch
+    feats = r.features()
+    for f in feats[::7]:
+        g = pickle.loads(pickle.dumps(f))
+        assert type(g) is F.Feature
+        assert g == f and g.fields == f.fields and g.fields_names == f.fields_names

@@ -1,8 +1,12 @@
-"""The headline path at its full size (BASELINE.json configs[4], bench.py's N = 8 per-GPU share):
-rank 0's LPT share of the 256-file C1-shaped directory (32 files, ~16.8 M records, ~0.99 GB)
-resident in HBM, decoded exactly as bench.py times it (key table and record-shape templates learned
-from a 4,096-record host sample, ShardDecoder.decode_device over two streams), then every value
-checked against what the deterministic generator wrote, record by record, vectorised:
+"""The headline path at its full size (BASELINE.json configs[4]), decoded exactly as bench.py times it
+(key table and record-shape templates learned from a 4,096-record host sample, the shard resident in
+HBM, ShardDecoder.decode_device over two streams), then every value checked against what the
+deterministic generator wrote, record by record, vectorised:
+
+* bench.py's N = 8 per-GPU share: rank 0's LPT share of the 256-file C1-shaped directory (32 files,
+  ~16.8 M records, ~0.99 GB) in the library's default 1 GiB batches;
+* bench.py's N = 1 batch plan: the first files of the directory, > 2 GiB, in the bench's 2 GiB
+  batches (one full 2 GiB batch of ~36 M records, batch offsets up to 2^31 - 2, plus the rest);
 
 * status OK and verdict 7 (length field, length CRC and payload CRC all match) for every record;
 * the dict order of every record: ``label`` first, ``id`` second (reader order, decoder.pyx:107-199);
@@ -34,25 +38,25 @@ def _expected_ids(f: int, n: int, lo: int, hi: int) -> np.ndarray:
     return out
 
 
-def test_headline_share_full_size_values():
+def _check(mine: list[int], batch_bytes: int | None) -> None:
     import torch
 
-    sizes = synth.c4_file_sizes(N_FILES, "c1")
-    mine = shard.lpt_partition(sizes, WORLD)[0]
     imgs = [synth.c4_file(f, "c1") for f in mine]
     sb = shard.ShardBatch([synth.c4_file_name(f) for f in mine], imgs)
     del imgs
     n = len(sb)
-    assert n > 15_000_000
     dev = torch.device("cuda", 0)
-    sd = shard.ShardDecoder(0)
+    sd = shard.ShardDecoder(0, batch_bytes) if batch_bytes else shard.ShardDecoder(0)
     try:
         plan = sd.plan(sb.starts, sb.ends, sb.nbytes)
+        if batch_bytes:
+            assert int((plan[:, 3] - plan[:, 2]).max()) > batch_bytes - 64  # a full batch of the bench's size
         rst, ren = sd.rebase(plan, sb.starts, sb.ends)
         d_bytes = torch.zeros(((sb.nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
         d_bytes[: sb.nbytes].copy_(torch.from_numpy(sb.buf))
         d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
         d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        del rst, ren
         sd.learn(plan, sb.buf, sb.starts, sb.ends)
         assert all(d.template_count() >= 1 for d in sd.decs)
         streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
@@ -60,6 +64,7 @@ def test_headline_share_full_size_values():
                          streams=[s.cuda_stream for s in streams])
         infos = sd.infos(plan)
         assert not any(i.n_miss_records or i.n_errors for i in infos)
+        del d_bytes, d_st, d_en
         res = sd.fetch(plan, sb.buf, sb.starts, sb.ends)
     finally:
         sd.close()
@@ -99,3 +104,16 @@ def test_headline_share_full_size_values():
             assert np.array_equal(got, want), (r0, c0)
         checked += m
     assert checked == n
+
+
+def test_headline_share_full_size_values():
+    sizes = synth.c4_file_sizes(N_FILES, "c1")
+    mine = [int(f) for f in shard.lpt_partition(sizes, WORLD)[0]]
+    _check(mine, None)
+
+
+def test_headline_2gib_batch_plan_values():
+    """bench.py's N = 1 plan: 2 GiB batches on two streams, one of them full (~36 M records)."""
+    sizes = synth.c4_file_sizes(N_FILES, "c1")
+    k = int(np.searchsorted(np.cumsum(sizes), (1 << 31) + (1 << 28))) + 1  # > 2.25 GiB of files
+    _check(list(range(k)), 1 << 31)

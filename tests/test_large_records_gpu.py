@@ -1,5 +1,5 @@
-"""k_stage_count: records above lane_max whose span fits the 12 KiB stage, counted one wavefront per
-record from LDS (entry-parallel canonical walk + lane-parallel payload CRC-32C), vs the oracle.
+"""Records above lane_max: walked from HBM by the lane kernel (one lane per record), payload CRC-32C
+by the streaming CRC (k_tail_count role 2), values by the wavefront gathers, vs the oracle.
 
 * the C3 config as defined (8,192 wide-schema records), some with corrupted length field, length
   CRC, payload or data CRC: status, values, key order and both CRC verdicts record by record;
@@ -10,8 +10,7 @@ record from LDS (entry-parallel canonical walk + lane-parallel payload CRC-32C),
   value holding a complete fake map entry (a false entry-start candidate that passes the per-entry
   checks: the chain check sends the record to the exact walker), a non-canonical kind;
 * every payload length / alignment around the CRC slice boundaries (192-byte lane slices);
-* the same batches with the kernel off (a record bound <= lane_max: the lane kernel's HBM walk)
-  give identical columns.
+* the same batches decoded as lane records (default lane_max) give identical columns.
 """
 
 import struct
@@ -59,13 +58,11 @@ def test_c3_config_with_corrupted_crcs(orc):
     b = _corrupt(buf, st, en)
     d = hip.HipDecoder(0)
     try:
-        d.set_stage_count(True)
         r = d.decode(b, st, en)
         assert r.info.n_big == 8192
         bad = _compare_to_oracle(r, orc, b, st, en)
         assert not bad, bad[:10]
-        # the same batch through the lane kernel's HBM walk (k_stage_count not launched)
-        d.set_stage_count(False)
+        # the same batch from device memory
         import torch
 
         dev = torch.device("cuda", 0)
@@ -78,7 +75,6 @@ def test_c3_config_with_corrupted_crcs(orc):
         r2 = d._fetch(b, st, en, info, False)
         for name in ("status", "verdict", "order", "row_splits", "i64", "f32"):
             assert np.array_equal(getattr(r, name), getattr(r2, name)), name
-        d.set_stage_count(True)
         strict = d.decode(b, st, en, strict_crc=True)
     finally:
         d.close()
@@ -99,9 +95,9 @@ def test_c3_config_with_corrupted_crcs(orc):
 
 @pytest.mark.parametrize("templates", [True, False])
 def test_small_records_forced_large_spec_placement(orc, templates):
-    """C1 records above a lane_max of 32: two slots placed speculatively (DevSchema::spec) by
-    k_stage_count, serial CRC of short payloads; a few records irregular (an extra id value, a
-    missing label) so the placement of their slot is withdrawn."""
+    """C1 records above a lane_max of 32: two slots placed speculatively (DevSchema::spec) by the
+    HBM walk, serial CRC of short payloads; a few records irregular (an extra id value, a missing
+    label) so the placement of their slot is withdrawn."""
     pl = synth.c1_payloads(3000)
     for i in range(5, 3000, 401):
         pl[i] = example(entry(b"label", i64(i % 1000)), entry(b"id", byt(b"img-x", b"y")))
@@ -110,14 +106,12 @@ def test_small_records_forced_large_spec_placement(orc, templates):
     buf, st, en = synth.framed(pl)
     d = hip.HipDecoder(0)
     try:
-        d.set_stage_count(True)
         d.set_templates(templates)
         d.set_lane_max(32)
         r = d.decode(buf, st, en)
         assert r.info.n_big == 3000
         assert not _compare_to_oracle(r, orc, buf, st, en)
         d.set_lane_max(hip.DEFAULT_LANE_MAX)
-        d.set_stage_count(False)
         base = d.decode(buf, st, en)
         assert _columns(base) == _columns(r)
     finally:
@@ -139,7 +133,6 @@ def test_records_the_parallel_walk_must_not_accept(orc):
     buf, st, en = synth.framed(pl)
     d = hip.HipDecoder(0)
     try:
-        d.set_stage_count(True)
         d.set_lane_max(64)
         r = d.decode(buf, st, en)
         assert not _compare_to_oracle(r, orc, buf, st, en)
@@ -161,7 +154,6 @@ def test_crc_slices_every_length(orc):
         b[int(st[i]) + 12 + (i * 131) % (int(en[i]) - int(st[i]) - 16)] ^= 0x10
     d = hip.HipDecoder(0)
     try:
-        d.set_stage_count(True)
         d.set_lane_max(64)
         r = d.decode(b, st, en)
         assert int(r.info.n_big) == len(pl)

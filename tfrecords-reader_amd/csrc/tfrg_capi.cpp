@@ -57,6 +57,16 @@ struct DBuf {
 
 constexpr uint32_t kMissCap = 1u << 16;
 
+// CRC-32C byte tables, built once (thread-safe: contexts of several host threads learn templates)
+const CrcTables& crc_tables() {
+  static const CrcTables T = [] {
+    CrcTables t;
+    crc_make_tables(&t);
+    return t;
+  }();
+  return T;
+}
+
 }  // namespace tfrg
 
 using namespace tfrg;
@@ -68,7 +78,6 @@ struct tfrg_ctx {
   uint32_t lane_max = 2048;
   uint32_t wave_stage = 0xffffffffu;  // clamped to the kernel's stage size
   uint64_t record_bound = 0;  // tfrg_ctx_set_record_bound: no record above this (0 = unknown)
-  bool stage_count = false;   // tfrg_ctx_set_stage_count (env TFRG_STAGE_COUNT)
   uint64_t call_bound = 0;    // tfrg_decode_host: the bound of its own ranges (one call)
   int num_cus = 256;
   // constants
@@ -82,6 +91,7 @@ struct tfrg_ctx {
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
   DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum, crc_rec, crc_base, crc_part;
   DBuf dq, dq_cnt;  // deferred packed-int64 bodies (k_body_count)
+  DBuf lmask, rlist;  // k_tpl_lane's per-group miss masks and listed groups
   DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
   bool materialized = false;
   bool tsum_dirty = true;  // the scan words must be cleared before the next decode
@@ -97,11 +107,14 @@ struct tfrg_ctx {
   std::vector<int32_t> key_slot_h;  // [4 * key]: flags, slot per kind
   DBuf tpl;
   uint32_t n_tpl = 0;
+  uint32_t tpl_w = 0;  // window words of the templates (16 / 32 / 64)
+  std::vector<uint32_t> tpl_h;  // host copy of the template words
   bool tpl_learned = false;
   bool tpl_on = true;
   // speculative single-value placement (DevSchema::spec), derived from the templates
   std::vector<uint8_t> slot_kind_h;
   DBuf spec;
+  std::vector<uint32_t> spec_h;  // host copy (k_tpl_lane's placement targets)
   bool have_spec = false;
   bool spec_on = true;
   // optional per-stage HIP events (tfrg_ctx_set_profiling)
@@ -125,7 +138,6 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
-  if (const char* e = getenv("TFRG_STAGE_COUNT")) c->stage_count = atoi(e) != 0;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -134,9 +146,10 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
     return TFRG_E_HIP;
   }
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
-  // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC); consts: 64 lane shifts x^(128 l), 16 un-shifts x^(-8z) and
-  // 32 round shifts x^(8192 * 2^k)
-  std::vector<uint32_t> tab(8192 + 16384 + 2048 + 24 * 1024), cst(256);
+  // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC), ..., then at
+  // kLeanTabOff [32][256] slice-by-32 (k_tpl_lane's position tables); consts: 64 lane shifts
+  // x^(128 l), 16 un-shifts x^(-8z) and 32 round shifts x^(8192 * 2^k)
+  std::vector<uint32_t> tab(kLeanTabOff + 32 * 256), cst(128);
   CrcTables T;
   crc_make_tables(&T);
   memcpy(tab.data(), T.t, 4096);
@@ -162,9 +175,14 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   for (int l = 0; l < 64; ++l) cst[l] = gf_xpow8(16ull * l);
   for (int z = 0; z < 16; ++z) cst[64 + z] = gf_xpow8_inv((uint64_t)z);
   for (int k = 0; k < 32; ++k) cst[96 + k] = gf_xpow8(1024ull << k);  // x^(8192 * 2^k): round shifts
-  // k_stage_count: lane l's CRC slice ends 196 (63 - l) bytes before the padded payload end
-  for (int l = 0; l < 64; ++l) cst[128 + l] = gf_xpow8(196ull * (63 - l));
-  for (int l = 0; l < 64; ++l) cst[192 + l] = gf_xpow8(196ull * (63 - l) + 96);  // (its first 100 bytes)
+  // T_d[v] = U(0, v followed by d zero bytes), d < 32
+  for (int v = 0; v < 256; ++v) {
+    uint32_t x = T.t[0][v];
+    for (int d = 0; d < 32; ++d) {
+      tab[kLeanTabOff + d * 256 + v] = x;
+      x = (x >> 8) ^ T.t[0][x & 0xff];
+    }
+  }
   if (c->crc_tab.ensure(tab.size() * 4) != hipSuccess || c->consts.ensure(cst.size() * 4) != hipSuccess ||
       hipMemcpy(c->crc_tab.p, tab.data(), tab.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(c->consts.p, cst.data(), cst.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
@@ -185,7 +203,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
                  &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
                  &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec,
-                 &c->dq, &c->dq_cnt};
+                 &c->dq, &c->dq_cnt, &c->lmask, &c->rlist};
   for (DBuf* b : all) b->release();
   if (c->order_ev) (void)hipEventDestroy(c->order_ev);
   if (c->have_events)
@@ -198,12 +216,6 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
 int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
   if (!c) return TFRG_E_ARG;
   c->lane_max = lane_max;
-  return 0;
-}
-
-int tfrg_ctx_set_stage_count(tfrg_ctx* c, int on) {
-  if (!c) return TFRG_E_ARG;
-  c->stage_count = on != 0;
   return 0;
 }
 
@@ -340,6 +352,7 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.krec = c->krec.as<uint32_t>();
   s.tpl = c->tpl.as<uint32_t>();
   s.n_tpl = c->tpl_on ? c->n_tpl : 0u;
+  s.tpl_w = c->tpl_w;
   s.spec = c->tpl_on && c->spec_on && c->have_spec && c->n_tpl ? c->spec.as<uint32_t>() : nullptr;
   return s;
 }
@@ -377,7 +390,14 @@ struct Tpl {
 
 // The dict fast_walk (tfrg_kernels.hip) builds for this payload, as a template; false where
 // fast_walk would bail (or the shape does not fit a template).
-bool tpl_derive(const tfrg_ctx* c, const uint8_t* p, uint32_t L, Tpl& t) {
+// the host key table the templates are derived against (tfrg_set_schema's, or a test's)
+struct TplSchema {
+  const std::unordered_map<std::string, uint32_t>& key_id;
+  const std::vector<int32_t>& key_slot;  // [4 * key]: flags, slot per kind
+  const std::vector<uint8_t>& slot_kind;
+};
+
+bool tpl_derive(const TplSchema* c, const uint8_t* p, uint32_t L, Tpl& t) {
   if (L < 2 || L > kTplMaxL) return false;
   t.L = L;
   t.bytes.assign(p, p + L);
@@ -399,8 +419,8 @@ bool tpl_derive(const tfrg_ctx* c, const uint8_t* p, uint32_t L, Tpl& t) {
     const auto it = c->key_id.find(std::string((const char*)p + ko, kl));
     if (it == c->key_id.end()) return false;
     const uint32_t kid = it->second;
-    if (c->key_slot_h[4ull * kid] & 1) return false;  // invalid UTF-8 key: the exact path
-    const int32_t slot = c->key_slot_h[4ull * kid + kind];
+    if (c->key_slot[4ull * kid] & 1) return false;  // invalid UTF-8 key: the exact path
+    const int32_t slot = c->key_slot[4ull * kid + kind];
     if (slot < 0 || std::find(seen.begin(), seen.end(), kid) != seen.end()) return false;
     seen.push_back(kid);
     uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0;
@@ -457,15 +477,15 @@ bool tpl_derive(const tfrg_ctx* c, const uint8_t* p, uint32_t L, Tpl& t) {
   return !t.ent.empty();
 }
 
-}  // namespace
-
-extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
-                                    const uint64_t* h_end, uint32_t n, uint32_t flags) {
-  if (!c || (n && (!h_bytes || !h_start || !h_end))) return TFRG_E_ARG;
-  c->tpl_learned = true;
-  c->n_tpl = 0;
-  c->have_spec = false;
-  if (!c->n_keys) return 0;
+// Record shapes of a host sample -> window-form templates (tfrg_internal.h) + the speculative
+// placement words. Returns the template count (0: none).
+struct Learned {
+  std::vector<uint32_t> w, spec;
+  uint32_t W = 0;
+  bool have_spec = false;
+};
+uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                      const uint64_t* h_end, uint32_t n, uint32_t flags, Learned& out) {
   std::map<std::string, std::pair<uint32_t, Tpl>> seen;  // shape -> (records, template)
   Tpl t;
   const uint32_t lim = n < 4096u ? n : 4096u;
@@ -490,48 +510,9 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
   const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMax);
   if (!nt) return 0;
-  std::vector<uint32_t> w((size_t)nt * kTplWords, 0);
-  for (uint32_t k = 0; k < nt; ++k) {
-    const Tpl& x = *order[k].second;
-    uint32_t* d = &w[(size_t)k * kTplWords];
-    d[0] = x.L;
-    d[1] = (uint32_t)(x.ent.size() / 4);
-    d[2] = (x.L + 3) / 4;
-    memcpy(d + kTplBytes, x.bytes.data(), x.L);
-    memcpy(d + kTplMask, x.mask.data(), x.L);
-    memcpy(d + kTplEnt, x.ent.data(), x.ent.size() * 4);
-    d[kTplV0] = 0xffffffffu;
-    if (x.L >= 4) {  // the CRC shortcut of a matching record (tfrg_internal.h)
-      static CrcTables CT;
-      static bool ct_made = false;
-      if (!ct_made) {
-        crc_make_tables(&CT);
-        ct_made = true;
-      }
-      std::vector<uint8_t> f(x.L);
-      uint32_t v0 = x.L;
-      for (uint32_t i = 0; i < x.L; ++i) {
-        f[i] = (uint8_t)(x.bytes[i] & x.mask[i]) ^ (i < 4 ? 0xffu : 0u);
-        if (x.mask[i] != 0xffu && v0 == x.L) v0 = i;
-      }
-      const uint64_t L64 = x.L;
-      d[kTplCrcK] = crc_update_bytes(CT, 0u, f.data(), x.L);
-      d[kTplLenCrc] = tfrg_masked_crc32c(reinterpret_cast<const uint8_t*>(&L64), 8);
-      d[kTplV0] = v0;
-    }
-  }
-  HIP_TRY(hipSetDevice(c->device));
-  if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
-  if (c->tpl.ensure(w.size() * 4)) {
-    set_error("template allocation failed");
-    return TFRG_E_NOMEM;
-  }
-  HIP_TRY(hipMemcpy(c->tpl.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
-  c->n_tpl = nt;
   // speculative placement (DevSchema::spec): slots that are an inline single value in every kept
   // template, taken per kind in slot order up to the first slot of that kind that is not one (its
   // column base n * rank then holds whenever every record is regular)
-  const uint32_t S = c->n_slots;
   std::vector<uint32_t> seen_inline(S, 0), spec(S ? S : 1, 0);
   for (uint32_t k = 0; k < nt; ++k) {
     const Tpl& x = *order[k].second;
@@ -540,29 +521,159 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
       if (mode && slot < S) ++seen_inline[slot];
     }
   }
+  bool have_spec = false;
   uint32_t rank[4] = {0, 0, 0, 0};
   bool open[4] = {true, true, true, true};
   for (uint32_t k = 0; k < S; ++k) {
-    const uint32_t kd = c->slot_kind_h[k] & 3u;
+    const uint32_t kd = c->slot_kind[k] & 3u;
     if (!open[kd]) continue;
     if (seen_inline[k] == nt) {
       spec[k] = ((++rank[kd]) << 2) | kd;
-      c->have_spec = true;
+      have_spec = true;
     } else {
       open[kd] = false;
     }
   }
-  if (c->have_spec) {
-    if (c->spec.ensure((size_t)S * 4)) {
-      set_error("template allocation failed");
-      return TFRG_E_NOMEM;
+  // window form (tfrg_internal.h): the last 4 W bytes of every kept shape's framed record
+  uint32_t maxL = 0;
+  for (uint32_t k = 0; k < nt; ++k) maxL = std::max(maxL, order[k].second->L);
+  const uint32_t W = maxL + 16 <= 64 ? 16u : (maxL + 16 <= 128 ? 32u : 64u);
+  const CrcTables& CT = crc_tables();
+  std::vector<uint32_t> w((size_t)nt * kLtWords, 0);
+  for (uint32_t k = 0; k < nt; ++k) {
+    const Tpl& x = *order[k].second;
+    const uint32_t L = x.L;
+    uint32_t* d = &w[(size_t)k * kLtWords];
+    std::vector<uint8_t> Bm(4 * W, 0), Mm(4 * W, 0), Cm(4 * W, 0);
+    const uint32_t off = 4 * W - (L + 16);  // window byte of the record start
+    const uint64_t L64 = L;
+    const uint32_t lcrc = tfrg_masked_crc32c(reinterpret_cast<const uint8_t*>(&L64), 8);
+    for (int i = 0; i < 8; ++i) {
+      Bm[off + i] = (uint8_t)(L64 >> (8 * i));
+      Mm[off + i] = 0xffu;
     }
-    HIP_TRY(hipMemcpy(c->spec.p, spec.data(), (size_t)S * 4, hipMemcpyHostToDevice));
+    for (int i = 0; i < 4; ++i) {
+      Bm[off + 8 + i] = (uint8_t)(lcrc >> (8 * i));
+      Mm[off + 8 + i] = 0xffu;
+    }
+    std::vector<uint8_t> fixed(L);
+    for (uint32_t p = 0; p < L; ++p) {
+      fixed[p] = x.bytes[p] & x.mask[p];
+      Bm[off + 12 + p] = fixed[p];
+      Mm[off + 12 + p] = x.mask[p];
+      Cm[off + 12 + p] = (uint8_t)~x.mask[p];
+    }
+    auto word = [&](const std::vector<uint8_t>& v, uint32_t i) {
+      return (uint32_t)v[4 * i] | ((uint32_t)v[4 * i + 1] << 8) | ((uint32_t)v[4 * i + 2] << 16) |
+             ((uint32_t)v[4 * i + 3] << 24);
+    };
+    uint32_t crcw = 0, chain = W;
+    for (uint32_t i = 0; i < W; ++i) {
+      d[kLtWin + i] = word(Bm, i);
+      d[kLtWin + W + i] = word(Mm, i);
+      d[kLtWin + 2 * W + i] = word(Cm, i);
+      if (!word(Cm, i)) continue;
+      if (i + 9 < W) chain = std::min(chain, i);
+      else crcw |= 1u << (i - (W - 9));
+    }
+    if (chain < W) crcw |= 1u;  // the chain's state joins word W - 9
+    d[kLtL] = L;
+    d[kLtNe] = (uint32_t)(x.ent.size() / 4);
+    d[kLtCrcw] = crcw;
+    d[kLtChain] = chain;
+    d[kLtK] = ~crc_update_bytes(CT, 0xffffffffu, fixed.data(), L);  // CRC-32C with every variable bit 0
+    uint32_t present = 0;
+    for (size_t e = 0; e < x.ent.size(); e += 4) {
+      const uint32_t slot = x.ent[e] & 0xffffffu, mode = x.ent[e] >> 24;
+      const uint32_t a = x.ent[e + 3] & 0xffffu, b = x.ent[e + 3] >> 16;
+      uint32_t pos = a;  // mode 0: list location
+      if (mode == 1 || mode == 2) pos = off + 12 + a;                  // window byte of the value
+      else if (mode == 3) pos = (uint32_t)((int64_t)a - 4 - (int64_t)L);  // element = end + pos
+      const uint32_t sp = slot < S && spec[slot] ? 1u : 0u;
+      uint32_t* q = d + kLtEnt + e;  // (e steps by 4 words)
+      q[0] = (slot & 0xffu) | (mode << 8) | (sp << 12) | (b << 16);
+      q[1] = x.ent[e + 1];
+      q[2] = x.ent[e + 2];
+      q[3] = pos;
+      if (slot < 32) present |= 1u << slot;
+    }
+    d[kLtAbsent] = ~present & (S >= kLeanMaxSlots ? 0xffffu : ((1u << S) - 1u));
   }
+  out.w = std::move(w);
+  out.spec = std::move(spec);
+  out.W = W;
+  out.have_spec = have_spec;
+  return nt;
+}
+
+}  // namespace
+
+extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
+                                    const uint64_t* h_end, uint32_t n, uint32_t flags) {
+  if (!c || (n && (!h_bytes || !h_start || !h_end))) return TFRG_E_ARG;
+  c->tpl_learned = true;
+  c->n_tpl = 0;
+  c->have_spec = false;
+  if (!c->n_keys) return 0;
+  const TplSchema sch{c->key_id, c->key_slot_h, c->slot_kind_h};
+  Learned L;
+  const uint32_t nt = learn_shapes(&sch, c->n_slots, h_bytes, nbytes, h_start, h_end, n, flags, L);
+  if (!nt) return 0;
+  const uint32_t S = c->n_slots;
+  const std::vector<uint32_t>& w = L.w;
+  const bool have_spec = L.have_spec;
+  const std::vector<uint32_t>& spec = L.spec;
+  const uint32_t W = L.W;
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+  if (c->tpl.ensure(w.size() * 4) || (have_spec && c->spec.ensure((size_t)S * 4))) {
+    set_error("template allocation failed");
+    return TFRG_E_NOMEM;
+  }
+  HIP_TRY(hipMemcpy(c->tpl.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  if (have_spec) HIP_TRY(hipMemcpy(c->spec.p, spec.data(), (size_t)S * 4, hipMemcpyHostToDevice));
+  c->n_tpl = nt;
+  c->tpl_w = W;
+  c->tpl_h = w;
+  c->spec_h = spec;
+  c->have_spec = have_spec;
+  return (int)nt;
+}
+
+extern "C" int tfrg_learn_templates_host(uint32_t n_keys, const uint8_t* key_blob, const uint64_t* key_offsets,
+                                         const uint32_t* key_flags, uint32_t n_slots, const uint32_t* slot_key,
+                                         const uint8_t* slot_kind, const uint8_t* h_bytes, uint64_t nbytes,
+                                         const uint64_t* h_start, const uint64_t* h_end, uint32_t n, uint32_t flags,
+                                         uint32_t* out, uint64_t cap, uint32_t* window_words) {
+  if (n && (!h_bytes || !h_start || !h_end)) return TFRG_E_ARG;
+  std::unordered_map<std::string, uint32_t> key_id;
+  std::vector<int32_t> ks(4ull * (n_keys ? n_keys : 1), -1);
+  for (uint32_t k = 0; k < n_keys; ++k) {
+    key_id.emplace(std::string((const char*)key_blob + key_offsets[k], key_offsets[k + 1] - key_offsets[k]), k);
+    ks[4ull * k] = (int32_t)(key_flags ? (key_flags[k] & 1u) : 0u);
+  }
+  for (uint32_t s2 = 0; s2 < n_slots; ++s2) {
+    if (slot_key[s2] >= n_keys || slot_kind[s2] < 1 || slot_kind[s2] > 3) return TFRG_E_ARG;
+    ks[4ull * slot_key[s2] + slot_kind[s2]] = (int32_t)s2;
+  }
+  std::vector<uint8_t> sk(slot_kind, slot_kind + n_slots);
+  const TplSchema sch{key_id, ks, sk};
+  Learned L;
+  const uint32_t nt = learn_shapes(&sch, n_slots, h_bytes, nbytes, h_start, h_end, n, flags, L);
+  if (window_words) *window_words = L.W;
+  if (out && nt) memcpy(out, L.w.data(), std::min<uint64_t>(L.w.size(), cap) * 4);
   return (int)nt;
 }
 
 extern "C" int tfrg_template_count(tfrg_ctx* c) { return c ? (int)c->n_tpl : TFRG_E_ARG; }
+
+extern "C" int tfrg_template_words(tfrg_ctx* c, uint32_t* out, uint64_t cap, uint32_t* window_words) {
+  if (!c) return TFRG_E_ARG;
+  if (window_words) *window_words = c->tpl_w;
+  const uint64_t nw = (uint64_t)c->n_tpl * kLtWords;
+  if (out) memcpy(out, c->tpl_h.data(), (nw < cap ? nw : cap) * 4);
+  return (int)c->n_tpl;
+}
 
 extern "C" int tfrg_ctx_set_templates(tfrg_ctx* c, int on) {
   if (!c) return TFRG_E_ARG;
@@ -594,6 +705,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   }
   const uint32_t S = c->n_slots;
   const uint64_t nn = n ? n : 1;
+  const uint64_t ngroups = (nn + 63) / 64;  // k_tpl_lane's 64-record groups
   const uint32_t n_tiles = (n + kTileRecs - 1) / kTileRecs;
   const uint32_t tile_stride = (n_tiles + 3u) & ~3u;
   const uint32_t n_chunks = (n_tiles + (1u << kSpineChunkShift) - 1u) >> kSpineChunkShift;
@@ -611,7 +723,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
               c->rs.cap < S * (nn + 1) * 4 || c->i64.cap < cap_i64 * 8 || c->f32.cap < cap_f32 * 4 ||
               c->b_off.cap < cap_b * 4 || c->b_len.cap < cap_b * 4 || c->big_list.cap < nn * 4 ||
               c->slow_list.cap < nn * 4 || c->tsum.cap < tsum_words * 4 + 16 || c->crc_rec.cap < nn * 4 ||
-              c->crc_base.cap < nn * 8 || c->crc_part.cap < nn * 8;
+              c->crc_base.cap < nn * 8 || c->crc_part.cap < nn * 8 || c->lmask.cap < ngroups * 8 ||
+              c->rlist.cap < ngroups * 4;
   if (grow && c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
   const size_t tsum_cap0 = c->tsum.cap;
   if (c->status.ensure(nn * 4) || c->aux.ensure(nn * 8) || c->verdict.ensure(nn) || c->order.ensure(S * nn * 2) ||
@@ -621,7 +734,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->slow_list.ensure(nn * 4) ||
       c->miss.ensure(kMissCap * 16ull) || c->info.ensure(kInfoCount * 4) ||
       c->tsum.ensure(tsum_words * 4 + 16) || c->crc_rec.ensure(nn * 4) || c->crc_base.ensure(nn * 8) ||
-      c->crc_part.ensure(nn * 8)) {
+      c->crc_part.ensure(nn * 8) || c->lmask.ensure(ngroups * 8) || c->rlist.ensure(ngroups * 4)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
@@ -690,8 +803,12 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.crc_rec = c->crc_rec.as<uint32_t>();
   o.crc_base = c->crc_base.as<uint64_t>();
   o.crc_part = c->crc_part.as<uint64_t>();
+  o.lmask = c->lmask.as<uint64_t>();
+  o.rlist = c->rlist.as<uint32_t>();
   LaunchCfg cfg;
   cfg.num_cus = c->num_cus;
+  cfg.lean = c->tpl_on && c->n_tpl;
+  cfg.spec_h = c->spec_h.empty() ? nullptr : c->spec_h.data();
   const uint64_t lane_blocks = (n + 255) / 256;
   const uint64_t lane_cap = (uint64_t)c->num_cus * 8;
   cfg.lane_grid = (int)(lane_blocks < 1 ? 1 : (lane_blocks < lane_cap ? lane_blocks : lane_cap));
@@ -700,10 +817,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
   cfg.lane_max = c->lane_max;
   cfg.wave_stage = c->wave_stage;
-  // k_stage_count only when a record above lane_max may exist (its empty launch costs microseconds)
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
-  cfg.stage_count = c->stage_count && (bound == 0 || bound > c->lane_max);
   // deferred packed bodies when records above lane_max may be walked from HBM: one 64-row block
   // (2,048 entries of 16 bytes) per 256 KiB of input, at least 16
   o.dq = nullptr;
@@ -796,12 +911,12 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
     if (b > a) total += b - a;
     if (h_end[i] > a && h_end[i] - a > widest) widest = h_end[i] - a;
   }
-  c->cap_hint = total;
-  c->call_bound = widest ? widest : 1;
   if (!c->tpl_learned && c->n_keys && c->tpl_on) {  // record shapes of the first host batch of a schema
     const int t = tfrg_learn_templates(c, h_bytes, nbytes, h_start, h_end, n, flags);
     if (t < 0) return t;
   }
+  c->cap_hint = total;
+  c->call_bound = widest ? widest : 1;
   return tfrg_decode_device(c, c->in_bytes.as<uint8_t>(), nbytes, c->in_start.as<uint64_t>(),
                             c->in_end.as<uint64_t>(), n, flags, st);
 }
@@ -831,6 +946,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   for (int k = 0; k < 4; ++k) info->kind_totals[k] = kt[k];
   info->nbytes = c->nbytes;
   info->bytes_data_len = blen;
+  info->tpl_groups_missed = h[kInfoResid];
   if (h[kInfoOverflow]) {
     set_error("value columns overflowed their capacity (overlapping ranges in a device batch): decode "
               "the ranges from host memory (tfrg_decode_host) or split the batch");

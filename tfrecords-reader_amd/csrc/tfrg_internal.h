@@ -20,8 +20,9 @@ struct DevSchema {
   const uint8_t* slot_kind;    // [n_slots]
   const uint32_t* key_w;       // [n_keys][2]: first / last 4 key bytes (see key_hash_words)
   const uint32_t* krec;        // [n_keys][8] packed key record, see KeyRec
-  const uint32_t* tpl;         // [n_tpl][kTplWords] record-shape templates (below), learned on the host
+  const uint32_t* tpl;         // [n_tpl][kLtWords] record-shape templates in window form (below)
   uint32_t n_tpl;
+  uint32_t tpl_w;              // their window words W (16, 32 or 64)
   // [n_slots] speculative placement of single values (null = off): 0, or (rank + 1) << 2 | kind for
   // a slot that is an inline single value in every learned template, as are all slots of its kind
   // before it. The lane kernel then writes such a value straight to its column at n * rank + r and
@@ -33,18 +34,47 @@ struct DevSchema {
 // Record-shape template: the payload of a canonical record whose every byte except list contents is
 // fixed (keys, tags, lengths, entry order; for packed int64 lists the continuation bits, i.e. the
 // varint boundaries). A record equal to it under the mask has exactly the template's dict (slots,
-// ranks, counts, list locations): the lane kernel then skips the canonical walk and reads only the
-// inline values. Layout (u32 words): [0] payload length L, [1] entries, [2] ceil(L/4), [3] 0,
-// [4, 4+64) bytes, [68, 68+64) mask, [132, 132+4*16) entries {slot | mode << 24, rank, count word,
-// a | b << 16}; mode 0: loc (a, b) = (list offset, list length), 1: inline int64 varint at a of b
-// bytes, 2: inline float at a, 3: inline bytes element at a of b bytes.
-// [196] K = U(0, (bytes & mask) with its first 4 bytes inverted) over the L bytes, [197] the masked
-// CRC-32C of the 8 length bytes of L, [198] v0 = the first payload byte with a variable bit
-// (0xffffffff: no CRC shortcut, L < 4). A matching record M = (bytes & mask) ^ V, V = M & ~mask, so
-// its CRC-32C is ~(K ^ U(0, V[v0, L))) (U linear, crc32c.h): only the bytes from v0 on are read.
-constexpr uint32_t kTplMaxL = 256, kTplMaxEntries = 16, kTplMax = 4;
-constexpr uint32_t kTplBytes = 4, kTplMask = 68, kTplEnt = 132, kTplCrcK = 196, kTplLenCrc = 197, kTplV0 = 198,
-                   kTplWords = 200;
+// ranks, counts, list locations), which k_tpl_lane (tfrg_tpl.hip) writes without a walk. Learned on
+// the host (tfrg_learn_templates) and stored in WINDOW form: the last 4 W bytes of the framed record,
+// [end - 4 W, end), as W little-endian words, so that the length field, its masked CRC, the payload
+// and the stored data CRC (word W - 1) sit at template-constant positions for every record of the
+// shape. Per window word: Bm = fixed bytes & mask, Mm = mask (0 outside the record, for the data
+// CRC and for variable payload bits), Cm = the variable payload bits (the CRC's input). Payload
+// byte p of a length-L record is window byte y = p + 4 W - 4 - L, at distance d = 4 W - 5 - y from
+// the payload end; d < 32 for words W - 9 .. W - 2.
+// Layout (u32): [kLtL] L, [kLtNe] entries, [kLtCrcw] bit j: word W - 9 + j has variable payload
+// bits, [kLtChain] first word < W - 9 with variable payload bits (W: none), [kLtK] CRC-32C of the
+// payload with every variable bit 0, [kLtAbsent] slots (< kLeanMaxSlots) absent from the shape,
+// [kLtEnt + 4 e] entries {slot | mode << 8 | spec << 12 | len << 16, rank, count word, pos}; mode 0:
+// list location (pos = payload offset, len), 1: inline int64 varint of len bytes at window byte pos,
+// 2: inline float at window byte pos, 3: inline bytes element of len bytes, pos = payload offset -
+// 4 - L (the element's batch offset is end + pos); [kLtWin, +W) Bm, [+W, +2W) Mm, [+2W, +3W) Cm.
+constexpr uint32_t kTplMaxL = 240, kTplMaxEntries = 16, kTplMax = 4;
+constexpr uint32_t kLtMaxW = 64;
+constexpr uint32_t kLtL = 0, kLtNe = 1, kLtCrcw = 2, kLtChain = 3, kLtK = 4, kLtAbsent = 5, kLtEnt = 8,
+                   kLtWin = kLtEnt + 4 * kTplMaxEntries, kLtWords = kLtWin + 3 * kLtMaxW;
+constexpr uint32_t kLeanMaxSlots = 16;  // k_tpl_lane runs for schemas of at most this many slots
+constexpr uint32_t kLeanTabOff = 51200;  // crc_tab words: T_d, d < 32, 256 entries each (slice-by-32)
+
+// Column targets of one slot for k_tpl_lane, computed on the host per decode.
+struct LeanTgt {
+  uint16_t* ord;   // order column of the slot
+  uint32_t* cnt;   // count column
+  uint2* loc;      // loc column
+  uint32_t* rs;    // row-split column (speculative placement)
+  void* v1;        // speculative placement: value column at n * (rank - 1) (int64 / float bits / bytes offset)
+  uint32_t* v2;    // speculative placement of bytes: the length column at n * (rank - 1)
+  uint32_t lim;    // speculative placement: records r < lim are stored (capacity)
+  uint32_t kind;   // speculative placement kind (0: the slot is not placed speculatively)
+  uint32_t tsum;   // slot * tile_stride
+  uint32_t pad;
+};
+struct LeanArgs {
+  uint32_t n_tpl;
+  uint32_t lane_max;
+  uint32_t* tsum;
+  LeanTgt tg[kLeanMaxSlots];
+};
 
 // Packed per-key record (8 x u32) staged into LDS by the lane kernels' fast path.
 enum KeyRec : uint32_t { kKrHash = 0, kKrLen, kKrW0, kKrW1, kKrSlot1, kKrSlot2, kKrSlot3, kKrFlags, kKrWords };
@@ -100,6 +130,7 @@ enum InfoIdx : uint32_t {
   kInfoBytesBig = 13,    // k_bytes_scan: long elements listed for the wave copy
   kInfoCrcCtr = 14,      // [14..15] u64: streaming-CRC list entries << kCrcIdxShift | flat 1 KiB rounds
   kInfoDefer = 16,       // k_lane_count: 64-record rows of deferred packed-int64 bodies reserved (k_body_count)
+  kInfoResid = 17,       // k_tpl_lane: 64-record groups listed for k_lane_count (records no template took)
   kInfoCount = 20
 };
 
@@ -112,8 +143,8 @@ constexpr uint32_t kDeferK = 32;
 constexpr int32_t kStatusRedo = 0x7fff0001;
 
 // verdict byte of a record the lane kernel left to the exact walker (k_tail_count role 1 writes its
-// final verdict, payload CRC included); role 2 (payload CRCs of large records) skips such records,
-// so the two roles of one launch never write the same verdict byte
+// final verdict, payload CRC included); role 2 (payload CRCs of large records) never lists such
+// records (a record k_body_count sends back is on both lists: role 2 ORs its bit in atomically)
 constexpr uint32_t kVerdictPending = 0x80u;
 
 // streaming payload CRC of the large records (k_tail_count role 2)
@@ -159,6 +190,8 @@ struct DevOut {
   uint4* dq;             // [dq_blocks][64][kDeferK] deferred bodies (nullptr: no deferral this decode)
   uint8_t* dq_cnt;       // [dq_blocks][64] entries used per row (0 for records not accepted)
   uint32_t dq_blocks;
+  uint64_t* lmask;       // [groups] k_tpl_lane: per 64-record group, the records it did not take (null: not run)
+  uint32_t* rlist;       // [groups] k_tpl_lane: the groups with such records (null: k_lane_count takes all)
 };
 
 // Row-split scan tiles: 256 consecutive records (one lane-kernel workgroup iteration)
@@ -198,20 +231,23 @@ uint64_t materialize_lb_words(uint64_t cap_b);
 // launchers (tfrg_kernels.hip)
 struct LaunchCfg {
   int num_cus;
+  bool lean;               // k_tpl_lane first (window-form templates, framed records with CRCs)
+  const uint32_t* spec_h;  // host copy of DevSchema::spec (k_tpl_lane's placement targets)
   int lane_grid;           // cap: workgroups for one record per lane
   int wave_grid;
   uint32_t lane_max;       // records above this size go to the wave kernels
   uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
-  bool stage_count;        // the batch may hold staged records above lane_max: launch k_stage_count
   bool body_count;         // deferred packed bodies possible (DevOut::dq): launch k_body_count
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
-enum Stage : int { kStageLaneCount = 0, kStageStageCount, kStageBodyCount, kStageTailCount, kStageSpine,
+enum Stage : int { kStageTplLane = 0, kStageLaneCount, kStageBodyCount, kStageTailCount, kStageSpine,
                    kStageDownGather, kStageTailGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.
+hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* tpl, uint32_t w,
+                           const uint32_t* d_tab, int num_cus, hipStream_t st);
 hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant);
 hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
                          const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream,

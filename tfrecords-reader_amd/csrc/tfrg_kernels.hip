@@ -24,6 +24,7 @@
 #include <type_traits>
 #include "tfrg_internal.h"
 #include "crc32c.h"
+#include "tfrg_walk.h"
 #include "../../include/tfrg_status.h"
 
 namespace tfrg {
@@ -112,228 +113,6 @@ struct LdsSrc {
   }
 };
 
-// decode_varint (decoder.pyx:34-50). COMPAT reproduces the reference's int-width shift:
-// term = (int32)((b & 0x7F) << (shift & 31)), sign-extended.
-template <bool COMPAT, class S>
-__device__ __forceinline__ int rd_varint(S& s, int64_t& pos, int64_t& val) {
-  int64_t r = 0;
-  int shift = 0;
-  for (;;) {
-    const uint32_t b = s.at(pos);
-    ++pos;
-    const uint32_t g = b & 0x7fu;
-    if (COMPAT) {
-      r |= (int64_t)(int32_t)(g << (shift & 31));
-    } else if (shift < 64) {
-      r |= (int64_t)((uint64_t)g << shift);
-    }
-    if (!(b & 0x80u)) break;
-    shift += 7;
-    if (shift >= 64) return TFRG_ERR_VARINT_TOO_MANY;
-  }
-  if (s.ub) return TFRG_UB_READ_PAST_END;
-  val = r;
-  return TFRG_OK;
-}
-
-// same control flow without assembling the value (counting passes)
-template <class S>
-__device__ __forceinline__ int skip_varint(S& s, int64_t& pos) {
-  int shift = 0;
-  for (;;) {
-    const uint32_t b = s.at(pos);
-    ++pos;
-    if (!(b & 0x80u)) break;
-    shift += 7;
-    if (shift >= 64) return TFRG_ERR_VARINT_TOO_MANY;
-  }
-  return s.ub ? TFRG_UB_READ_PAST_END : TFRG_OK;
-}
-
-struct Fld {
-  int64_t fn, wt, off, len;
-};
-
-// One iteration of decode_message (decoder.pyx:69-104).
-template <bool COMPAT, class S>
-__device__ __forceinline__ int rd_field(S& s, int64_t& pos, int64_t end, Fld& f, int64_t& aux) {
-  int64_t key;
-  int st = rd_varint<COMPAT>(s, pos, key);
-  if (st) return st;
-  f.fn = key >> 3;
-  f.wt = key & 7;
-  if (f.wt == 1) {
-    if (pos + 8 > end) return TFRG_ERR_EOB_FIXED64;
-    f.off = pos;
-    f.len = 8;
-    pos += 8;
-    return TFRG_OK;
-  }
-  if (f.wt == 2) {
-    int64_t len;
-    st = rd_varint<COMPAT>(s, pos, len);
-    if (st) return st;
-    if (COMPAT) {
-      if (pos + len > end) return TFRG_ERR_EOB_LEN;  // |len| < 2^31 here: no overflow
-      if (len < 0) return TFRG_UB_NEGATIVE_LENGTH;   // passes the check, then pos moves back
-    } else {
-      if (pos > end || (uint64_t)len > (uint64_t)(end - pos)) return TFRG_ERR_EOB_LEN;
-    }
-    f.off = pos;
-    f.len = len;
-    pos += len;
-    return TFRG_OK;
-  }
-  if (f.wt == 5) {
-    if (pos + 4 > end) return TFRG_ERR_EOB_FIXED32;
-    f.off = pos;
-    f.len = 4;
-    pos += 4;
-    return TFRG_OK;
-  }
-  aux = f.wt;
-  return TFRG_ERR_WIRE_TYPE;
-}
-
-// decode_message validation pass: every tag/length of one level before any child is parsed,
-// which is the reference's level-by-level error precedence.
-template <bool COMPAT, class S>
-__device__ int scan_msg(S& s, int64_t pos, int64_t end, int64_t& aux) {
-  Fld f;
-  while (pos < end) {
-    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
-    if (st) return st;
-  }
-  return TFRG_OK;
-}
-
-// bytes/float/int64 list (decoder.pyx:203-300): validation + element count.
-template <bool COMPAT, class S>
-__device__ int list_count(S& s, int kind, int64_t o, int64_t n, int64_t& aux, uint32_t& count) {
-  const int64_t end = o + n;
-  int st = scan_msg<COMPAT>(s, o, end, aux);
-  if (st) return st;
-  uint64_t c = 0;
-  int64_t pos = o;
-  Fld f;
-  while (pos < end) {
-    rd_field<COMPAT>(s, pos, end, f, aux);  // validated above
-    if (f.fn != 1) continue;
-    if (kind == TFRG_KIND_BYTES) {
-      if (f.wt != 2) return TFRG_ERR_WT_BYTES_LIST;
-      ++c;
-    } else if (kind == TFRG_KIND_FLOAT) {
-      if (f.wt == 2) c += (uint64_t)(f.len >> 2);  // floor(len/4): trailing bytes dropped
-      else if (f.wt == 5) ++c;
-      else return TFRG_ERR_WT_FLOAT_LIST;
-    } else {
-      if (f.wt != 2) return TFRG_ERR_WT_INT64_LIST;
-      // packed varints until p >= chunk end; the last one may run past the chunk (no bound)
-      int64_t p = f.off;
-      const int64_t e = f.off + f.len;
-      while (p < e) {
-        st = skip_varint(s, p);
-        if (st) return st;
-        ++c;
-      }
-    }
-  }
-  count = (uint32_t)c;
-  return TFRG_OK;
-}
-
-// feature_from_bytes (decoder.pyx:169-199): kind = field number of the FIRST field.
-template <bool COMPAT, class S>
-__device__ int walk_feature(S& s, int64_t o, int64_t n, int64_t& aux, int& kind, int64_t& lo,
-                            int64_t& ll, uint32_t& count) {
-  const int64_t end = o + n;
-  int64_t pos = o;
-  Fld f, g0;
-  int cnt = 0;
-  while (pos < end) {
-    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
-    if (st) return st;
-    if (cnt == 0) g0 = f;
-    ++cnt;
-  }
-  if (cnt == 0) return TFRG_UB_EMPTY_FEATURE;
-  if (g0.fn < 1 || g0.fn > 3) return TFRG_ERR_FEATURE_FIELD;
-  kind = (int)g0.fn;
-  lo = g0.off;
-  ll = g0.len;
-  return list_count<COMPAT>(s, kind, g0.off, g0.len, aux, count);
-}
-
-// parse_map_entry (decoder.pyx:153-166): positional fields[0] = key, fields[1] = value.
-template <bool COMPAT, class S, class Sink>
-__device__ int walk_entry(S& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
-  const int64_t end = o + n;
-  int64_t pos = o;
-  Fld f, f0, f1;
-  int cnt = 0;
-  while (pos < end) {
-    const int st = rd_field<COMPAT>(s, pos, end, f, aux);
-    if (st) return st;
-    if (cnt == 0) f0 = f;
-    else if (cnt == 1) f1 = f;
-    ++cnt;
-  }
-  if (cnt < 2) return TFRG_UB_SHORT_MAP_ENTRY;
-  const int kid = sink.lookup(s, f0.off, f0.len);
-  // An unknown key may be invalid UTF-8, which would raise before the feature is parsed: report
-  // it now (kind 0 = key only) so the next round can rank this record's errors correctly.
-  if (kid == -1) sink.note_miss(0, f0.off, f0.len);
-  if (kid == -2) {  // interned as invalid UTF-8: bytes(key).decode('utf-8') raises here
-    aux = (int64_t)(((uint64_t)f0.off << 32) | (uint64_t)(uint32_t)f0.len);
-    return TFRG_ERR_KEY_UTF8;
-  }
-  int kind = 0;
-  int64_t lo = 0, ll = 0;
-  uint32_t count = 0;
-  const int st = walk_feature<COMPAT>(s, f1.off, f1.len, aux, kind, lo, ll, count);
-  if (st) return st;
-  return sink.insert(kid, kind, lo, ll, count, f0.off, f0.len);
-}
-
-// features_from_bytes (decoder.pyx:130-150)
-template <bool COMPAT, class S, class Sink>
-__device__ int walk_features(S& s, Sink& sink, int64_t o, int64_t n, int64_t& aux) {
-  const int64_t end = o + n;
-  int st = scan_msg<COMPAT>(s, o, end, aux);
-  if (st) return st;
-  sink.reset();  // a repeated Features field replaces the dict, never merges (decoder.pyx:121)
-  int64_t pos = o;
-  Fld f;
-  while (pos < end) {
-    rd_field<COMPAT>(s, pos, end, f, aux);
-    if (f.fn != 1) continue;
-    if (f.wt != 2) return TFRG_ERR_WT_FEATURE;
-    st = walk_entry<COMPAT>(s, sink, f.off, f.len, aux);
-    if (st) return st;
-  }
-  return TFRG_OK;
-}
-
-// example_from_bytes (decoder.pyx:107-127) + Feature(proto.features.feature) (feature.py:106)
-template <bool COMPAT, class S, class Sink>
-__device__ int walk_example(S& s, Sink& sink, int64_t& aux) {
-  const int64_t L = s.L;
-  int st = scan_msg<COMPAT>(s, 0, L, aux);
-  if (st) return st;
-  bool have = false;
-  int64_t pos = 0;
-  Fld f;
-  while (pos < L) {
-    rd_field<COMPAT>(s, pos, L, f, aux);
-    if (f.fn != 1) continue;
-    if (f.wt != 2) return TFRG_ERR_WT_FEATURES;
-    st = walk_features<COMPAT>(s, sink, f.off, f.len, aux);
-    if (st) return st;
-    have = true;
-  }
-  return have ? TFRG_OK : TFRG_ERR_FEATURES_NONE;
-}
-
 // ------------------------------------------------------------------------------------------------
 // Count sink: dict semantics (insertion order, last value wins, first position kept) over
 // (key, kind) slots, with the per-record rank state in LDS.
@@ -355,15 +134,6 @@ __device__ __forceinline__ void put_inline(const DevOut& o, uint32_t kind, uint2
     o.b_off[dst] = lc.x;
     o.b_len[dst] = lc.y;
   }
-}
-
-// DevSchema::spec word of a wave-uniform slot, in an SGPR (TFRG_TPL_SMEM: HBM, else the LDS copy)
-__device__ __forceinline__ uint32_t spec_word_u(const uint32_t* spec, uint32_t slot) {
-#if TFRG_TPL_SMEM
-  return ((cu32*)spec)[slot];
-#else
-  return __builtin_amdgcn_readfirstlane(spec[slot]);
-#endif
 }
 
 // Speculative placement target of one slot (DevSchema::spec), staged in LDS by the lane kernel's
@@ -403,27 +173,17 @@ __device__ __forceinline__ void spec_target(uint32_t* dst, const DevOut& o, uint
 }
 
 // put_inline at a staged target (record r of the batch)
-// Column stores of the lane kernel: written once, never re-read by it (TFRG_NT_STORES = 1: with the
-// nontemporal hint, a measured-only build option)
-#ifndef TFRG_NT_STORES
-#define TFRG_NT_STORES 0
-#endif
-template <class T>
-__device__ __forceinline__ void st_col(T* p, T v) {
-  if constexpr (TFRG_NT_STORES) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
 __device__ __forceinline__ void put_spec(const lds_spec_t* t, uint2 lc, uint32_t r) {
   const spec_u32x4 a = t[0], b = t[1];
   if (r >= b.x) return;
   const uint64_t p1 = ((uint64_t)a.y << 32) | a.x;
   if (b.y == TFRG_KIND_INT64) {
-    st_col(reinterpret_cast<uint64_t*>(p1) + r, ((uint64_t)lc.y << 32) | lc.x);
+    reinterpret_cast<uint64_t*>(p1)[r] = ((uint64_t)lc.y << 32) | lc.x;
   } else if (b.y == TFRG_KIND_FLOAT) {
-    st_col(reinterpret_cast<uint32_t*>(p1) + r, lc.x);
+    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
   } else {
-    st_col(reinterpret_cast<uint32_t*>(p1) + r, lc.x);
-    st_col(reinterpret_cast<uint32_t*>(((uint64_t)a.w << 32) | a.z) + r, lc.y);
+    reinterpret_cast<uint32_t*>(p1)[r] = lc.x;
+    reinterpret_cast<uint32_t*>(((uint64_t)a.w << 32) | a.z)[r] = lc.y;
   }
 }
 
@@ -444,7 +204,6 @@ struct CountSinkT {
   cnt_t* cnt = nullptr;  // LDS value counts, same layout as ord (L only)
   const lds_u32* spec = nullptr;  // DevSchema::spec staged in LDS (L only; null = off)
   const lds_spec_t* spec_t = nullptr;  // its targets (kSpecTgtWords per slot)
-  const uint32_t* spec_u = nullptr;       // DevSchema::spec for uniform slots (scalar reads, as TplRef)
 
   __device__ __forceinline__ void reset() {
     for (uint32_t k = 0; k < sc->n_slots; ++k) ord[(size_t)k * ostride] = 0;
@@ -555,22 +314,6 @@ struct CountSinkT {
     o->loc[at] = lv;
   }
 
-  // fast_put at a wave-uniform slot / rank / count word (template entries): the speculative
-  // placement test is a scalar branch
-  __device__ __forceinline__ void fast_put_u(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
-    if constexpr (L) {
-      ord[(size_t)slot * ostride] = (uint16_t)rk;
-      cnt[(size_t)slot * ostride] = cw;
-      if (spec_u && (cw & kCountInline) && spec_word_u(spec_u, slot)) {
-        put_spec(spec_t + 2u * slot, lv, r);
-        return;
-      }
-      o->loc[(size_t)slot * n + r] = lv;
-    } else {
-      fast_put(slot, rk, cw, lv);
-    }
-  }
-
   // final count of a present slot (LDS, or read back from this thread's own column write)
   __device__ __forceinline__ uint32_t count_of(uint32_t k) const {
     if constexpr (L) return cnt[(size_t)k * ostride];
@@ -624,9 +367,6 @@ struct MaskSink {
     o->loc[at] = lv;
     pm |= 1ull << slot;
     __atomic_fetch_add(&tsl[slot], cw & ~kCountInline, __ATOMIC_RELAXED);
-  }
-  __device__ __forceinline__ void fast_put_u(uint32_t slot, uint32_t rk, uint32_t cw, uint2 lv) {
-    fast_put(slot, rk, cw, lv);
   }
   __device__ __forceinline__ void rollback() {  // this thread's own column writes, read back
     for (uint64_t m = pm; m; m &= m - 1) {
@@ -783,13 +523,7 @@ __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
 // Kernels
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneBlock = 256;
-#ifndef TFRG_LANE_BLOCK
-#define TFRG_LANE_BLOCK 256
-#endif
-constexpr int kLaneCountBlock = TFRG_LANE_BLOCK;  // k_lane_count workgroup (its LDS tables are per workgroup)
-#ifndef TFRG_LANE_MINB
-#define TFRG_LANE_MINB 6  // waves per SIMD the (LDS-dict) count kernel is register-budgeted for
-#endif
+constexpr int kLaneCountBlock = 256;  // k_lane_count workgroup (its LDS tables are per workgroup)
 constexpr int kWaveBlock = 256;
 constexpr int kWavesPerBlock = kWaveBlock / 64;
 
@@ -820,10 +554,7 @@ __device__ __forceinline__ bool strict_pass(const DevBatch& B, uint32_t verdict,
 // with coalesced 16-byte loads (1 KiB per wave-instruction) and every lane then parses its record
 // from LDS instead of issuing scattered, latency-bound global loads.
 // ------------------------------------------------------------------------------------------------
-#ifndef TFRG_STAGE_BYTES
-#define TFRG_STAGE_BYTES 4096
-#endif
-constexpr uint32_t kStageBytes = TFRG_STAGE_BYTES;    // span capacity per wave
+constexpr uint32_t kStageBytes = 4096;   // span capacity per wave
 constexpr uint32_t kStageStride = kStageBytes + 64;   // + slack for aligned over-reads at the tail
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t x) {
@@ -873,10 +604,7 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-#ifndef TFRG_WSTAGE
-#define TFRG_WSTAGE 12288
-#endif
-constexpr uint32_t kWStage = TFRG_WSTAGE;           // staged record bytes per wave (wavefront kernels)
+constexpr uint32_t kWStage = 12288;          // staged record bytes per wave (wavefront kernels)
 constexpr uint32_t kWStageStride = kWStage + 64;
 
 // copy absolute bytes [lo16, hi) (lo16 16-aligned, wave-uniform, hi - lo16 <= kStageBytes) into dst
@@ -929,10 +657,7 @@ __device__ __forceinline__ uint32_t crc_head_state(uint32_t k) {
   // ~0 (x) x^(-8k) for k = 0..3 (checked against crc32c("123456789") with k zero bytes prepended)
   return k == 0 ? 0xffffffffu : (k == 1 ? 0xa942e6bcu : (k == 2 ? 0x2804363bu : 0x96db52a8u));
 }
-#ifndef TFRG_LANE_SLICE
-#define TFRG_LANE_SLICE 4  // slicing width of the lane kernel's CRC (4: 4 KiB of tables, 8: 8 KiB)
-#endif
-constexpr int kLaneSlice = TFRG_LANE_SLICE;
+constexpr int kLaneSlice = 4;  // slicing width of the lane kernel's CRC (4 KiB of tables)
 
 template <int R>
 __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint32_t b, const LdsTab<R>& T) {
@@ -941,23 +666,16 @@ __device__ __forceinline__ uint32_t crc_lds8(const uint8_t* l, uint32_t a, uint3
   uint32_t p = a & ~3u;
   uint32_t c = crc_head_state(k);
   uint32_t hm = 0xffffffffu << (8u * k);  // masks the bytes before a in the first dword
-  if constexpr (kLaneSlice == 8) {
-    for (; p + 8 <= bw; p += 8) {
-      c = T.step8(c ^ (w[p >> 2] & hm), w[(p >> 2) + 1]);
-      hm = 0xffffffffu;
-    }
-  } else {  // slice-by-4: the smaller table leaves LDS for more resident waves
-    for (; p + 12 <= bw; p += 8) {  // two words per iteration (one ds_read2, half the loop overhead)
-      const uint32_t x0 = w[p >> 2], x1 = w[(p >> 2) + 1];
-      c = T.step4(c ^ (x0 & hm));
-      hm = 0xffffffffu;
-      c = T.step4(c ^ x1);
-    }
-    if (p + 8 <= bw) {
-      c = T.step4(c ^ (w[p >> 2] & hm));
-      hm = 0xffffffffu;
-      p += 4;
-    }
+  for (; p + 12 <= bw; p += 8) {  // two words per iteration (one ds_read2, half the loop overhead)
+    const uint32_t x0 = w[p >> 2], x1 = w[(p >> 2) + 1];
+    c = T.step4(c ^ (x0 & hm));
+    hm = 0xffffffffu;
+    c = T.step4(c ^ x1);
+  }
+  if (p + 8 <= bw) {
+    c = T.step4(c ^ (w[p >> 2] & hm));
+    hm = 0xffffffffu;
+    p += 4;
   }
   if (p + 4 <= bw) {
     c = T.step4(c ^ (w[p >> 2] & hm));
@@ -1156,9 +874,6 @@ __device__ __forceinline__ bool count_packed(const S& s, uint32_t o, uint32_t e,
   return true;
 }
 
-#ifndef TFRG_HBM_BLOCKS
-#define TFRG_HBM_BLOCKS 2
-#endif
 // bit 7 of the 16 bytes of a block, byte i -> bit i
 __device__ __forceinline__ uint32_t cont16(uint4 b) {
   auto nib = [](uint32_t w) {
@@ -1190,12 +905,8 @@ __device__ __forceinline__ void packed_block(uint4 blk, uint32_t lo, uint32_t hi
 // round trips; four blocks per round would cost the staged path its occupancy in VGPRs)
 // (NB blocks per round: k_body_count, whose lanes count independent bodies, takes 8: one round for
 // a body of up to ~112 bytes)
-template <int NB = TFRG_HBM_BLOCKS, bool WIN>
+template <int NB = 2, bool WIN>
 __device__ __forceinline__ bool count_packed(const FastSrcG<WIN>& s, uint32_t o, uint32_t e, uint32_t& cnt) {
-#ifdef TFRG_DIAG_NOCOUNT  // diagnostic build (timing only, wrong counts): no loads of packed bodies
-  cnt = (e - o) >> 2;
-  return true;
-#endif
   uint32_t run = 0, terms = 0;
   const uint64_t a0 = s.base + o, a1 = s.base + e;
   // last block to load: the chunk's last one (spare loads of a round re-read it: no line past the
@@ -1518,177 +1229,13 @@ __device__ __forceinline__ int fast_walk(const S& s, const LdsKeys& K, Sink& sin
   return ok ? TFRG_OK : kBail;
 }
 
-// Record-shape templates (tfrg_internal.h, learned on the host) are read through the constant
-// address space: every template word is indexed by wave-uniform values (template, word, entry), so
-// the loads are scalar (s_load into SGPRs, the VALU operands directly) and the loop bounds, the
-// CRC start word and the entry modes are scalar branches, not exec-mask regions.
-#ifndef TFRG_TPL_SMEM
-#define TFRG_TPL_SMEM 0
-#endif
-#ifndef TFRG_TPL_SPLIT
-#define TFRG_TPL_SPLIT 1  // template match and template CRC as two loops (0: one fused loop)
-#endif
-// One template's words. Control words (lengths, entry fields, CRC constants) are wave-uniform:
-// u() returns them in SGPRs, so the loops and mode tests over them are scalar branches; d() reads
-// the per-word bytes / mask as VALU operands. TFRG_TPL_SMEM = 1 reads them with scalar loads from
-// HBM, 0 from the copy staged in LDS (a broadcast read, then v_readfirstlane for u()).
-struct TplRef {
-#if TFRG_TPL_SMEM
-  cu32* p;
-  __device__ __forceinline__ uint32_t u(uint32_t i) const { return p[i]; }
-  __device__ __forceinline__ uint32_t d(uint32_t i) const { return p[i]; }
-#else
-  const uint32_t* p;
-  __device__ __forceinline__ uint32_t u(uint32_t i) const { return __builtin_amdgcn_readfirstlane(p[i]); }
-  __device__ __forceinline__ uint32_t d(uint32_t i) const { return p[i]; }
-#endif
-  __device__ __forceinline__ TplRef at(uint32_t t) const { return TplRef{p + t * kTplWords}; }
-};
-
-// match result of one lane
-struct TplHit {
-  int t = -1;          // the first template the payload equals under its mask, -1 none
-  bool pc = false;     // pcrc holds the payload CRC-32C (the template defines v0)
-  uint32_t pcrc = 0;   // CRC-32C of the payload: ~(K ^ U(0, (M & ~mask)[v0, L)))
-  uint32_t lcrc = 0;   // masked CRC-32C of the 8 length bytes of L (a template constant)
-};
-
-// Templates in order, each over the lanes whose payload length is its L and that matched none
-// before it (a wave-uniform loop; a template no lane can match costs one ballot). The words the
-// match reads also feed the CRC of the variable bits from the template's first variable byte on
-// (crc = false: the match alone). The payload words come from the aligned stage words, one LDS
-// read per word (the previous one carried, one alignbyte).
-template <int R>
-__device__ __forceinline__ TplHit tpl_match_u(const FastSrc& fs, bool cand0, TplRef tg, uint32_t n_tpl,
-                                              const LdsTab<R>& T, bool crc) {
-  TplHit h;
-  const uint32_t* SW = reinterpret_cast<const uint32_t*>(fs.l) + (fs.p >> 2);
-  const uint32_t sh = fs.p & 3u;
-  for (uint32_t t = 0; t < n_tpl; ++t) {
-    const TplRef Tp = tg.at(t);
-    const uint32_t L = Tp.u(0);
-    // (an opaque copy of L: inside the branch below the compiler would otherwise substitute the
-    // lane's own length for it and keep the CRC's byte counts in VGPRs)
-    uint32_t Lu = L;
-    asm("" : "+s"(Lu));
-    const bool cand = cand0 && h.t < 0 && fs.L == L;
-    if (__ballot(cand) == 0) continue;
-    if (cand) {
-      const uint32_t nw = Tp.u(2), v0 = Tp.u(kTplV0);
-      const bool pc = crc && v0 != 0xffffffffu;
-      const uint32_t w0 = pc ? v0 >> 2 : nw;
-      uint32_t diff = 0, c = 0, prev = SW[0];
-#if TFRG_TPL_SPLIT
-      // the match over every word (no per-word CRC tests: scalar work is half the kernel's issue),
-      // then the CRC of the variable words in a counted loop of its own (they are read again)
-      for (uint32_t w = 0; w < nw; w += 4u) {
-        uint32_t x[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t next = SW[w + 1u + i];
-          x[i] = __builtin_amdgcn_alignbyte(next, prev, sh);
-          prev = next;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) diff |= (x[i] ^ Tp.d(kTplBytes + w + i)) & Tp.d(kTplMask + w + i);
-      }
-      if (pc) {
-        const uint32_t nfull = Lu >> 2, rem = Lu & 3u;
-        uint32_t pv = SW[w0];
-        for (uint32_t wi = w0; wi < nfull; ++wi) {
-          const uint32_t next = SW[wi + 1u];
-          const uint32_t x = __builtin_amdgcn_alignbyte(next, pv, sh);
-          pv = next;
-          c = T.step4(c ^ (x & ~Tp.d(kTplMask + wi)));
-        }
-        if (rem) {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
-          const uint32_t x = __builtin_amdgcn_alignbyte(SW[nfull + 1u], pv, sh);
-          const uint32_t y = c ^ (x & ~Tp.d(kTplMask + nfull) & bytes_mask(rem));
-          uint32_t u = T(rem - 1u, y & 0xffu);
-          if (rem >= 2u) u ^= T(rem - 2u, (y >> 8) & 0xffu);
-          if (rem == 3u) u ^= T(0u, (y >> 16) & 0xffu);
-          c = u ^ (c >> (8u * rem));
-        }
-      }
-#else
-      // four words per step: template words beyond L are zero (mask 0), the stage has 64 bytes of
-      // slack past any record
-      for (uint32_t w = 0; w < nw; w += 4u) {
-        uint32_t x[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t next = SW[w + 1u + i];
-          x[i] = __builtin_amdgcn_alignbyte(next, prev, sh);
-          prev = next;
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) diff |= (x[i] ^ Tp.d(kTplBytes + w + i)) & Tp.d(kTplMask + w + i);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t wi = w + i;
-          if (wi >= w0 && wi < nw) {  // (scalar branch)
-            const uint32_t m = Tp.d(kTplMask + wi), rem = Lu - 4u * wi;
-            if (rem >= 4u) {
-              c = T.step4(c ^ (x[i] & ~m));
-            } else {  // the last 1..3 payload bytes: one partial slicing step (as crc_lds8)
-              const uint32_t y = c ^ (x[i] & ~m & bytes_mask(rem));
-              uint32_t u = T(rem - 1u, y & 0xffu);
-              if (rem >= 2u) u ^= T(rem - 2u, (y >> 8) & 0xffu);
-              if (rem == 3u) u ^= T(0u, (y >> 16) & 0xffu);
-              c = u ^ (c >> (8u * rem));
-            }
-          }
-        }
-      }
-#endif
-      if (!diff) {
-        h.t = (int)t;
-        h.pc = pc;
-        h.pcrc = ~(c ^ Tp.u(kTplCrcK));
-        h.lcrc = Tp.u(kTplLenCrc);
-      }
-    }
-  }
-  return h;
-}
-
-// The matched template's dict, exactly as fast_walk builds it for this record: slots, ranks and
-// count words from the template (scalar), list locations or the inline values read from the record.
-template <class Sink>
-__device__ __forceinline__ void tpl_put_u(const FastSrc& fs, TplRef Tp, Sink& sink) {
-  const uint32_t ne = Tp.u(1);
-  for (uint32_t e = 0; e < ne; ++e) {
-    const uint32_t dx = Tp.u(kTplEnt + 4u * e), dy = Tp.u(kTplEnt + 4u * e + 1u), dz = Tp.u(kTplEnt + 4u * e + 2u),
-                   dw = Tp.u(kTplEnt + 4u * e + 3u);
-    const uint32_t mode = dx >> 24, a = dw & 0xffffu, b = dw >> 16;
-    uint2 lv;
-    if (mode == 0u) lv = make_uint2(a, b);                                       // (list offset, length)
-    else if (mode == 1u) lv = make_uint2(vgroups(fs.u32(a), bytes_mask(b)), 0u);  // one int64 varint
-    else if (mode == 2u) lv = make_uint2(fs.u32(a), 0u);                          // one float
-    else lv = make_uint2((uint32_t)(fs.base + a), b);                             // one bytes element
-    sink.fast_put_u(dx & 0xffffffu, dy, dz, lv);
-  }
-  sink.rank = ne;
-}
-
-// tpl_put_u for every lane with put set, template by template (wave-uniform loop)
-template <class Sink>
-__device__ __forceinline__ void tpl_put_all(const FastSrc& fs, bool put, int t_hit, TplRef tg, uint32_t n_tpl,
-                                            Sink& sink) {
-  for (uint32_t t = 0; t < n_tpl; ++t) {
-    const bool mine = put && t_hit == (int)t;
-    if (__ballot(mine) == 0) continue;
-    if (mine) tpl_put_u(fs, tg.at(t), sink);
-  }
-}
-
 // Framing verdicts of one record: length field vs the given range, masked CRC-32C of the 8 length
 // bytes and of the payload (the TFRecord spec; absent from the reference), from the
 // wave's LDS stage (STAGED) or from HBM.
 // payload_crc = false leaves the payload CRC of a record above lane_max to k_wave_count.
 template <int R, bool STAGED>
 __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, const LdsTab<R>& T, const uint8_t* stage,
-                                               uint64_t lo16, bool payload_crc = true, const TplHit* th = nullptr) {
+                                               uint64_t lo16, bool payload_crc = true) {
   if (B.flags & kFlagPayloadOnly) return;
   const bool do_crc = !(B.flags & kFlagNoCrc);
   const uint64_t D = v.e - v.st;
@@ -1708,10 +1255,8 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
     uint32_t want, stored;
     if constexpr (STAGED) {
       stored = lds_u32u(stage, (uint32_t)(v.st - lo16) + 8);
-      // a template's length: the masked CRC of its 8 length bytes is a constant of the template;
-      // else the two words just read, two slicing steps at any alignment
-      want = th && th->t >= 0 && lenf == (uint64_t)v.L ? th->lcrc
-                                                        : crc_mask(~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1));
+      // the two words just read: two slicing steps at any alignment
+      want = crc_mask(~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1));
     } else {
       want = crc_mask(crc_serial<R>(B.bytes, v.st, v.st + 8, T));
       stored = load_u32_unaligned(B.bytes, v.st + 8);
@@ -1721,8 +1266,7 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   if (do_crc && payload_crc && D >= 16) {
     uint32_t c, stored;
     if constexpr (STAGED) {
-      c = th && th->t >= 0 && th->pc ? th->pcrc
-                                     : crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
+      c = crc_lds8<R>(stage, (uint32_t)(v.p0 - lo16), (uint32_t)(v.e - 4 - lo16), T);
       stored = lds_u32u(stage, (uint32_t)(v.e - 4 - lo16));
     } else {
       c = crc_serial<R>(B.bytes, v.p0, v.e - 4, T);
@@ -1787,100 +1331,24 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
   return ((uint64_t)rfl32((uint32_t)(x >> 32)) << 32) | rfl32((uint32_t)x);
 }
 
-#ifndef TFRG_LANE_PREF
-#define TFRG_LANE_PREF 0  // lane kernel staging: 0 synchronous, 1 next span in registers, 2 next span by LDS-DMA
-#endif
-constexpr uint32_t kLaneBufs = TFRG_LANE_PREF == 2 ? 2u : 1u;  // stages per wave
-// The lane kernel's staging decision for one wave's records, from their offsets alone: the span of
-// the records the lane walk takes (fast path, <= lane_max), staged when it fits kStageBytes.
-__device__ __forceinline__ bool lane_span(const DevBatch& B, uint64_t st, uint64_t en, bool valid, bool fast_ok,
-                                          uint32_t lane_max, uint64_t& lo16, uint64_t& hi) {
-  bool sr = false;
-  uint64_t a = 0, b = 0;
-  if (valid) {
-    const RecView v = rec_view_se(B, st, en);
-    sr = fast_ok && v.status == TFRG_OK && v.e - v.st <= lane_max;
-    a = v.st;
-    b = v.e;
-  }
-  uint64_t lo;
-  wave_span(sr, a, b, lo, hi);
-  lo = rfl64(lo);
-  hi = rfl64(hi);
-  lo16 = lo & ~15ull;
-  return hi > lo && hi - lo16 <= kStageBytes;
-}
-
-// One wave's lane-kernel span (<= 4 KiB) held in registers between its loads and its LDS stores:
-// the next iteration's bytes are requested before this iteration's records are decoded.
-struct Pref4 {
-  uint4 w0, w1, w2, w3;
-};
-__device__ __forceinline__ Pref4 pref_load4(const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
-  static_assert(kStageBytes == 4096, "pref_load4 holds a 4 KiB span");
-  const uint8_t* base = src + lo16;
-  const uint32_t n = (uint32_t)(hi - lo16), o = lane * 16u;
-  // (loads past the span re-read its first line)
-  Pref4 p;
-  p.w0 = *reinterpret_cast<const uint4*>(base + (o < n ? o : 0u));
-  p.w1 = *reinterpret_cast<const uint4*>(base + (o + 1024u < n ? o + 1024u : 0u));
-  p.w2 = *reinterpret_cast<const uint4*>(base + (o + 2048u < n ? o + 2048u : 0u));
-  p.w3 = *reinterpret_cast<const uint4*>(base + (o + 3072u < n ? o + 3072u : 0u));
-  return p;
-}
-__device__ __forceinline__ void pref_store4(const Pref4& p, uint8_t* dst, uint64_t lo16, uint64_t hi, uint32_t lane) {
-  const uint32_t n = (uint32_t)(hi - lo16), o = lane * 16u;
-  if (o < n) *reinterpret_cast<uint4*>(dst + o) = p.w0;
-  if (o + 1024u < n) *reinterpret_cast<uint4*>(dst + o + 1024u) = p.w1;
-  if (o + 2048u < n) *reinterpret_cast<uint4*>(dst + o + 2048u) = p.w2;
-  if (o + 3072u < n) *reinterpret_cast<uint4*>(dst + o + 3072u) = p.w3;
-}
-
-// LDS byte address of a pointer into shared memory
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-// Copies absolute bytes [lo16, hi) (hi - lo16 <= kStageBytes) into the stage dst by LDS-DMA:
-// global_load_lds_dwordx4 writes lane l's 16 bytes at M0 + 16 l, one 1 KiB piece per
-// wave-instruction, with no VGPR destination. Lanes past the span re-read the piece's first line
-// (their bytes land past the span, inside the stage). The loads are inline asm, outside the
-// compiler's s_waitcnt bookkeeping: the caller waits vmcnt(0) before reading dst (an asm load
-// only ever makes the compiler's own in-order vmcnt waits stricter).
-__device__ __forceinline__ void dma_span(uint8_t* dst, const uint8_t* src, uint64_t lo16, uint64_t hi, uint32_t lane) {
-  const uint32_t n = rfl32((uint32_t)(hi - lo16));
-  const uint8_t* base = src + rfl64(lo16);
-  const uint32_t d0 = rfl32(lds_addr(dst));
-  for (uint32_t k = 0; k < n; k += 1024u) {  // (wave-uniform)
-    const uint32_t off = k + lane * 16u;
-    const uint8_t* g = base + (off < n ? off : k);
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g), "s"(d0 + k)
-        : "memory");
-  }
-}
-__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-
-// Lane-per-record FAST path. Each wave copies the contiguous span of its 64 records into its LDS
-// stage, then every lane checks its record's framing + CRC and runs the single-pass canonical walker
-// (fast_walk). Records the fast walker does not accept (non-canonical, erroneous, unknown keys), records
-// of a wave whose span does not fit the stage and framing errors are listed for k_slow_count; records
-// above lane_max for the wavefront kernels. The per-slot value counts of the accepted records are
-// summed per 256-record tile (first level of the row-split scan).
-// GORD: dict state in the global order/count columns (key tables too large for the LDS budget).
-// MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns (GORD).
+// Lane-per-record kernel, the general path. Each wave copies the contiguous span of its 64 records
+// into its LDS stage, then every lane checks its record's framing + CRC and runs the single-pass
+// canonical walker (fast_walk). Records the fast walker does not accept (non-canonical, erroneous,
+// unknown keys) and framing errors are listed for the exact walker (k_tail_count role 1); records
+// above lane_max, and the lane records of a wave whose span does not fit the stage, are walked from
+// HBM. The per-slot value counts of the accepted records are summed per 256-record tile (first level
+// of the row-split scan).
+// Residual mode (DevOut::rlist set): only the records k_tpl_lane did not take, i.e. the 64-record
+// groups it listed, each with its miss mask (DevOut::lmask).
+// MODE: 0 = per-lane dict in LDS, 1 = MaskSink (<= 64 slots), 2 = dict in the global columns.
 template <int R, bool COMPAT, int MODE>
-__global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
-                                                                           const uint32_t* __restrict__ crc_tab,
-                                                                           uint32_t lane_max, uint32_t wave_stage,
-                                                                           uint32_t stage_cnt) {
+__global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
+                                                                                  const uint32_t* __restrict__ crc_tab,
+                                                                                  uint32_t lane_max, uint32_t wave_stage) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // slicing tables at a static LDS address: lookups fold the table base into the ds_read offset
   __shared__ uint32_t tab[256 * kLaneSlice * R];
+  constexpr uint32_t kWaves = kLaneCountBlock / 64;
   uint32_t* cnt = lds;                                       // [n_slots][kLaneCountBlock]
   constexpr bool GORD = MODE != 0;  // no per-lane LDS dict
   const uint32_t S = sc.n_slots;
@@ -1889,13 +1357,11 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
   const uint32_t ord_bytes = GORD ? 0u : ((S * kLaneCountBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint8_t* stage_all = reinterpret_cast<uint8_t*>(ord) + ord_bytes;
-  // (TFRG_LANE_PREF 2: two stages per wave, the next span's LDS-DMA lands in the other one)
-  uint8_t* stage_w = stage_all + wib * kLaneBufs * kStageStride;
-  uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + (kLaneCountBlock / 64) * kLaneBufs * kStageStride);
+  uint8_t* stage = stage_all + wib * kStageStride;
+  uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + kWaves * kStageStride);
   uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
-  uint32_t* tpl_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? (kLaneCountBlock / 64) * 64u : 0u);
-  uint32_t* spec_l = tpl_l + (TFRG_TPL_SMEM ? 0u : sc.n_tpl * kTplWords);  // MODE 0: DevSchema::spec
+  uint32_t* spec_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? kWaves * 64u : 0u);  // MODE 0: DevSchema::spec
   uint32_t* spec_tl = spec_l + ((S + 7u) & ~7u);  // MODE 0: its targets (16-byte aligned)
   for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneCountBlock) tab[i] = crc_tab[2048 + i / R];
   if constexpr (MODE == 1) {
@@ -1905,8 +1371,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
   if (fast_ok) {
     for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneCountBlock) kht[i] = sc.ht[i];
     for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneCountBlock) krec[i] = sc.krec[i];
-    if (!TFRG_TPL_SMEM)
-      for (uint32_t i = threadIdx.x; i < sc.n_tpl * kTplWords; i += kLaneCountBlock) tpl_l[i] = sc.tpl[i];
   }
   const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
   if (spec_on)
@@ -1918,82 +1382,47 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
   const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
 
-  // the next iteration's offsets are requested before this iteration's stores (one HBM round trip
-  // less on the critical path of the next iteration)
-  const uint64_t lstride = (uint64_t)gridDim.x * kLaneCountBlock;
-  uint64_t base = (uint64_t)blockIdx.x * kLaneCountBlock + wib * 64u;
+  // 64-record groups: group g of the batch, or (residual mode) the g-th listed group with its mask
+  const bool resid = o.rlist != nullptr;
+  const uint32_t nres = resid ? rfl32(o.info[kInfoResid]) : 0u;
+  const uint32_t nw = gridDim.x * kWaves;
+  auto group = [&](uint32_t g, uint64_t& gb, uint64_t& gm) -> bool {
+    if (resid) {
+      if (g >= nres) return false;
+      const uint32_t w = rfl32(o.rlist[g]);
+      gb = (uint64_t)w * 64u;
+      gm = rfl64(o.lmask[w]);
+      return true;
+    }
+    gb = (uint64_t)g * 64u;
+    gm = ~0ull;
+    return gb < B.n;
+  };
+  uint32_t g = blockIdx.x * kWaves + wib;
+  uint64_t base = 0, gmask = 0;
+  bool more = group(g, base, gmask);
+  // the next group's offsets are requested before this group's stores (one HBM round trip less on
+  // the critical path of the next group)
   uint64_t nst = 0, nen = 0;
-  if (base + lane < B.n) {
+  if (more && base + lane < B.n) {
     nst = B.start[base + lane];
     nen = B.end[base + lane];
   }
-#if TFRG_LANE_PREF
-  // the first iteration's span in flight, and the next iteration's offsets
-  uint64_t cst = nst, cen = nen, plo16 = 0, phi = 0;
-  bool pstaged = lane_span(B, cst, cen, base + lane < B.n, fast_ok, lane_max, plo16, phi);
-#if TFRG_LANE_PREF == 2
-  uint32_t buf = 0;
-  if (pstaged) dma_span(stage_w, B.bytes, plo16, phi, lane);
-#else
-  Pref4 pf{};
-  if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
-#endif
-  nst = nen = 0;
-  if (base + lstride + lane < B.n) {
-    nst = B.start[base + lstride + lane];
-    nen = B.end[base + lstride + lane];
-  }
-#endif
-  for (; base < B.n; base += lstride) {
+  while (more) {
     PHASE_MARK(p0);
     const uint64_t ri = base + lane;
-    const bool valid = ri < B.n;
+    const bool valid = ri < B.n && ((gmask >> lane) & 1ull);
     const uint32_t r = (uint32_t)ri;
-#if TFRG_LANE_PREF
-    const uint64_t cst0 = cst, cen0 = cen;
-    const uint64_t lo16 = plo16;
-    const bool staged = pstaged;
-#if TFRG_LANE_PREF == 2
-    // this span's DMA (issued one iteration ago) and the offsets loaded with it have landed; the
-    // wait also covers the previous iteration's stores (one counter)
-    wait_vm0();
-    uint8_t* stage = stage_w + buf * kStageStride;
-#else
-    uint8_t* stage = stage_w;
-    if (staged) {
-      pref_store4(pf, stage, lo16, phi, lane);
-      wave_lds_sync();
-    }
-#endif
-    {  // the next iteration's span: its loads in flight while this iteration decodes
-      const uint64_t rn = ri + lstride;
-      pstaged = lane_span(B, nst, nen, rn < B.n, fast_ok, lane_max, plo16, phi);
-#if TFRG_LANE_PREF == 2
-      if (pstaged) {
-        wait_lgkm0();  // (the other stage's last reads, one iteration ago, are complete)
-        dma_span(stage_w + (buf ^ 1u) * kStageStride, B.bytes, plo16, phi, lane);
-      }
-      buf ^= 1u;
-#else
-      if (pstaged) pf = pref_load4(B.bytes, plo16, phi, lane);
-#endif
-      cst = nst;
-      cen = nen;
-      if (rn + lstride < B.n) {
-        nst = B.start[rn + lstride];
-        nen = B.end[rn + lstride];
-      }
-    }
-#else
+    const uint32_t tile = (uint32_t)(base >> kTileShift);
     const uint64_t cst0 = nst, cen0 = nen;
-    if (ri + lstride < B.n) {
-      nst = B.start[ri + lstride];
-      nen = B.end[ri + lstride];
+    g += nw;
+    more = group(g, base, gmask);
+    if (more && base + lane < B.n) {
+      nst = B.start[base + lane];
+      nen = B.end[base + lane];
     }
-#endif
     RecView v{};
     bool mine = false;
-    bool stg = false;  // counted by k_stage_count (staged large record, launched for this batch)
     if (valid) {
       v = rec_view_se(B, cst0, cen0);
       const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
@@ -2001,7 +1430,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
         if (v.e - (v.st & ~15ull) <= wave_stage) {
           const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
           o.big_list[i] = r;
-          stg = stage_cnt != 0u;
         } else {
           const uint32_t i = atomicAdd(&o.info[kInfoHuge], 1u);
           o.big_list[B.n - 1u - i] = r;
@@ -2011,8 +1439,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
     }
     // wave-uniform staging decision over the span of this wave's records
     const bool span_rec = fast_ok && mine && v.status == TFRG_OK;
-#if !TFRG_LANE_PREF
-    uint8_t* stage = stage_w;
     uint64_t lo, hi;
     wave_span(span_rec, v.st, v.e, lo, hi);
     const uint64_t lo16 = lo & ~15ull;
@@ -2021,7 +1447,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
       stage_span(stage, B.bytes, lo16, hi, lane);
       wave_lds_sync();
     }
-#endif
     PHASE_MARK(p1);
     PHASE_ADD(16, p0, p1);
     using SinkT = std::conditional_t<MODE == 1, MaskSink, CountSinkT<MODE == 0>>;
@@ -2036,7 +1461,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
           if (spec_on) {
             c.spec = (const lds_u32*)spec_l;
             c.spec_t = (const lds_spec_t*)spec_tl;
-            c.spec_u = TFRG_TPL_SMEM ? sc.spec : spec_l;
           }
         }
         return c;
@@ -2045,25 +1469,13 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
     bool done = false;
     bool tried = false;
     if (staged && span_rec) {
-      // a known record shape (template) first: it also carries most of the record's CRC-32C work
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
-      const bool fcrc = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
-#if TFRG_TPL_SMEM
-      const TplRef tg{(cu32*)sc.tpl};
-#else
-      const TplRef tg{tpl_l};
-#endif
-      TplHit th;
-      if (sc.n_tpl) th = tpl_match_u<R>(fs, true, tg, sc.n_tpl, T, fcrc);
-      frame_verdicts<R, true>(B, v, T, stage, lo16, true, &th);
+      frame_verdicts<R, true>(B, v, T, stage, lo16, true);
       PHASE_MARK(p2);
       PHASE_ADD(17, p1, p2);
       sink.fast_reset(S);
-      const bool pass = strict_pass(B, v.verdict, true);  // (strict mode: a CRC failure is the slow kernel's)
-      // a known record shape: its dict without the walk
-      if (sc.n_tpl) tpl_put_all(fs, pass, th.t, tg, sc.n_tpl, sink);
-      if (pass) {
-        done = th.t >= 0 || fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
+      if (strict_pass(B, v.verdict, true)) {  // (strict mode: a CRC failure is the slow kernel's)
+        done = fast_walk<COMPAT>(fs, K, sink) == TFRG_OK;
         tried = true;
       }
       PHASE_MARK(p3);
@@ -2071,9 +1483,9 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
     }
     // records above lane_max, and lane records of a wave whose span does not fit the stage: the
     // canonical walk straight from HBM, one record per lane (64 latency chains in flight per wave).
-    // The payload CRC of records above lane_max is k_big_crc's streaming pass; the others' is
-    // computed here, serially per lane from HBM.
-    const bool bigw = fast_ok && valid && ((!mine && !stg) || (span_rec && !staged));
+    // The payload CRC of records above lane_max is the streaming CRC's (k_tail_count role 2); the
+    // others' is computed here, serially per lane from HBM.
+    const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));
     if (__ballot(bigw)) {
       // one block of deferred-body rows per wave (k_body_count), while the batch has room
       uint32_t blk = ~0u;
@@ -2104,7 +1516,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
     }
     PHASE_MARK(p4);
     // everything else of this wave's records goes to the exact walker
-    const bool slow = valid && !done && !stg;
+    const bool slow = valid && !done;
     const uint64_t sm = __ballot(slow);
     if (sm) {
       uint32_t b0 = 0;
@@ -2116,15 +1528,14 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
       }
     }
     if (done) {
-      st_col(o.status + r, (int32_t)TFRG_OK);
-      st_col(o.verdict + r, (uint8_t)v.verdict);
+      o.status[r] = TFRG_OK;
+      o.verdict[r] = (uint8_t)v.verdict;
     }
     // the payload CRC of an accepted large record: one entry of the streaming CRC list
     const bool crc_on = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
     const uint32_t crc_j =
         done && !mine && crc_on && v.e - v.st >= 16 && (uint64_t)v.L >= kCrcListMin ? crc_rounds_of(v.p0, v.e - 4) : 0u;
     // order / count columns of the accepted records + the tile sums (one atomic per slot and wave)
-    const uint32_t tile = (uint32_t)(base >> kTileShift);
     if constexpr (MODE == 1) {
       if (tried && !done) sink.rollback();
       if (done) sink.zero_absent(S);
@@ -2138,29 +1549,26 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? TFRG_LANE_MINB : 4) vo
       }
     }
     if constexpr (MODE != 1) {
-    for (uint32_t k = 0; k < S; ++k) {
-      const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
-      const uint32_t c = ov ? sink.count_of(k) : 0u;
-      if (done) {
-        const size_t at = (size_t)k * B.n + r;
-        st_col(o.order + at, (uint16_t)ov);
-#ifdef TFRG_DIAG_NOCNT  // diagnostic build: no count word for regular speculatively placed values
-        if (!(spec_on && spec_l[k] && mine && c == (1u | kCountInline)))
-#endif
-        st_col(o.count + at, c);
+      for (uint32_t k = 0; k < S; ++k) {
+        const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
+        const uint32_t c = ov ? sink.count_of(k) : 0u;
+        if (done) {
+          const size_t at = (size_t)k * B.n + r;
+          o.order[at] = (uint16_t)ov;
+          o.count[at] = c;
+        }
+        const uint32_t x = c & ~kCountInline;
+        const uint64_t nz = __ballot(x != 0u);
+        if (nz) {  // counts of 0/1 (single values): the sum is a popcount of the ballot (scalar)
+          const uint32_t t = __ballot(x > 1u) ? wave_sum_u32(x) : (uint32_t)__popcll(nz);
+          if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
+        }
+        if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
+          if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
+          const uint64_t irm = __ballot(valid && !(done && c == (1u | kCountInline)));
+          if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
+        }
       }
-      const uint32_t x = c & ~kCountInline;
-      const uint64_t nz = __ballot(x != 0u);
-      if (nz) {  // counts of 0/1 (single values): the sum is a popcount of the ballot (scalar)
-        const uint32_t t = __ballot(x > 1u) ? wave_sum_u32(x) : (uint32_t)__popcll(nz);
-        if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
-      }
-      if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
-        if (valid) st_col(o.rs + (size_t)k * (B.n + 1) + r, r);
-        const uint64_t irm = __ballot(valid && !stg && !(done && c == (1u | kCountInline)));
-        if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
-      }
-    }
     }
     crc_list_append(o, r, crc_j, lane);
     wave_lds_sync();  // the stage is rewritten by the next iteration
@@ -2195,10 +1603,7 @@ __device__ void withdraw_record(const DevOut& o, uint32_t n, uint32_t n_slots, u
 // and lists it for the exact walker (k_tail_count role 1), which withdraws the record's columns and
 // re-walks it.
 constexpr int kBodyBlock = 256;
-#ifndef TFRG_BODY_PARTS
-#define TFRG_BODY_PARTS 4
-#endif
-constexpr uint32_t kBodyParts = TFRG_BODY_PARTS;  // waves per block of rows (kDeferK / kBodyParts columns each)
+constexpr uint32_t kBodyParts = 4;  // waves per block of rows (kDeferK / kBodyParts columns each)
 __global__ __launch_bounds__(kBodyBlock) void k_body_count(DevBatch B, DevOut o) {
   const uint32_t nblk = o.info[kInfoDefer] < o.dq_blocks ? o.info[kInfoDefer] : o.dq_blocks;
   const uint32_t lane = threadIdx.x & 63u;
@@ -2315,29 +1720,6 @@ __device__ __forceinline__ bool hdr_0a(const FastSrc& s, uint32_t q, uint32_t& b
   return bo <= s.L && len <= s.L - bo;
 }
 
-// Finalize of a wavefront record: order/count columns and tile sums, one slot per lane. Counts come
-// from the wave's LDS dict, or (GORD) from the count column written by other lanes of this wave.
-template <class Sink>
-__device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink, uint32_t n_slots, uint32_t n,
-                                              uint32_t r, bool good, uint32_t lane) {
-  if constexpr (!Sink::kLds) __threadfence();
-  for (uint32_t k = lane; k < n_slots; k += 64) {
-    const uint32_t vv = good ? sink.ord[(size_t)k * sink.ostride] : 0u;
-    const size_t at = (size_t)k * n + r;
-    uint32_t c = 0;
-    if (vv) {
-      if constexpr (Sink::kLds) c = sink.cnt[(size_t)k * sink.ostride];
-      else c = __hip_atomic_load(&o.count[at], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    o.order[at] = (uint16_t)vv;
-    o.count[at] = c;
-    if (c & ~kCountInline) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + (r >> kTileShift)], c & ~kCountInline);
-  }
-}
-
-#ifndef TFRG_CRC_DEPTH
-#define TFRG_CRC_DEPTH 4
-#endif
 // Streaming payload CRC of the large records (k_tail_count role 2). The lane kernel lists every
 // accepted record above lane_max (crc_list_append) with its 1 KiB rounds counted into ONE flat
 // round space: list entry i owns the flat rounds [base_i, base_{i+1}); round j of a record,
@@ -2349,7 +1731,7 @@ __device__ __forceinline__ void wave_finalize(const DevOut& o, const Sink& sink,
 // rounds inside one wave are lane-combined (x^(128 l)) and shifted by x^(8192 jlo) to their place;
 // the slices of a record split over waves XOR together in crc_part (CRC-32C is linear, crc32c.h)
 // and the wave whose rounds complete the record finishes it.
-constexpr int kCrcDepth = TFRG_CRC_DEPTH;
+constexpr int kCrcDepth = 4;  // rounds of loads in flight per wave
 [[maybe_unused]] constexpr uint32_t kCstUnshift = 64;     // consts: [0, 64) x^(128 l), [64, 80) x^(-8z),
 [[maybe_unused]] constexpr uint32_t kCstRoundPow = 96;    // [96, 128) x^(8192 * 2^k)
 constexpr uint32_t kPowTabOff = 26624;   // crc_tab: [24][4][256] multiply by x^(8192 * 2^k) (split-slice shifts)
@@ -2658,7 +2040,10 @@ __device__ __forceinline__ void crc_flush(const uint8_t* lbase, const uint32_t* 
     v = xor3(rt(2u, v & 0xffu), rt(1u, (v >> 8) & 0xffu), rt(0u, (v >> 16) & 0xffu)) ^ rt(15u, v >> 24);
   for (; zz; --zz) v = (v >> 8) ^ rt(15u, v & 0xffu);
   if (v == t) {
-    if (lane == 0) o.verdict[r] = (uint8_t)(verdict | TFRG_V_DATA_CRC);
+    // one atomic OR on the byte's aligned word: a record k_body_count sent back to the exact walker
+    // (role 1 of the same launch) may have its verdict byte written by role 1 at the same time
+    if (lane == 0)
+      atomicOr(reinterpret_cast<uint32_t*>(o.verdict + (r & ~3u)), (uint32_t)TFRG_V_DATA_CRC << (8u * (r & 3u)));
   } else if (B.flags & kFlagStrictCrc) {
     strict_reject(o, B.n, n_slots, r, verdict, lane, 64);
   }
@@ -2871,8 +2256,11 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
 
 // The exception paths before the row-split scan in ONE launch (usually both empty: a workgroup leaves
 // at once when it has nothing to do): the exact walker for the slow list (role 1), then the streaming
-// payload CRC of the listed large records (role 2). The two record sets are disjoint (the lane kernel
-// lists only records it accepted), so a strict CRC rejection of role 2 never meets role 1's records.
+// payload CRC of the listed large records (role 2). The lane kernel lists only records it accepted,
+// but a listed record whose deferred packed body k_body_count rejected (kStatusRedo) is on role 1's
+// list too: role 2 then sets its DATA_CRC bit with an atomic OR on the verdict word (role 1 writes the
+// whole byte, with the same bit, at any time of the launch), and its strict rejection applies only to
+// a status still TFRG_OK (strict_reject), i.e. never to role 1's records.
 // (Role 2 as its own kernel at 5 instead of 4 waves per SIMD measured the same on C2: 0.129 vs 0.130
 // ms; its own launch cost every batch ~6.5 us.)
 // 512-thread blocks: the streaming CRC's 70 KiB of LDS tables then still leave 4 waves per SIMD.
@@ -2934,396 +2322,6 @@ __device__ __forceinline__ void pref_store(const Pref& p, uint8_t* dst, uint64_t
 }
 #undef TFRG_PREF_LOAD
 #undef TFRG_PREF_STORE
-
-// ------------------------------------------------------------------------------------------------
-// Records above lane_max whose span fits the stage (big_list[0, kInfoBig)): the count pass, one WAVE
-// per record, from ONE LDS copy of the record (k_stage_count, launched between k_lane_count and
-// k_tail_count when the batch may hold such records and the schema has <= 64 slots).
-//  * framing: the length field and the masked CRC-32C of its 8 bytes;
-//  * the payload CRC-32C, lane-parallel from the stage: lane l owns the 49 aligned words ending
-//    196 (63 - l) bytes before the payload's word-padded end (kSgQ x 64 >= the 12 KiB stage), a
-//    slice-by-8 chain from a zero state over them (the payload's first 4 bytes inverted: the ~0
-//    initial state, crc32c.h), placed by x^(8 * 196 (63 - l)) (gf_mul) and XOR-reduced over the
-//    wave; the z <= 3 zero bytes padding the last word are matched by advancing the stored CRC's
-//    state over z zero bytes (as role_crc_stream's flush);
-//  * fast_walk's canonical walk, ENTRY-PARALLEL: all lanes scan the Features body for entry starts
-//    (0x0a tag, 1- or 2-byte length, the key's 0x0a tag: every canonical entry, a few false
-//    positives), the candidates are compacted in position order and each is parsed by its own
-//    lane with fast_walk's per-entry checks; the parsed entries must chain from the body's start to
-//    its end (a false candidate surviving the checks, or a non-canonical record -> the exact
-//    walker), their chain positions are the ranks;
-//  * the dict (order / count / loc words, inline single values, speculative placement) and the
-//    tile sums, one slot per lane.
-// For these records it replaces the lane kernel's per-lane walk from HBM (one dependent HBM round
-// trip per entry header: C3's count pass was latency-bound at 1.9 TB/s) and their entry in the
-// streaming-CRC list (a second read of every payload).
-constexpr uint32_t kSgMaxSlots = 64;                 // one slot per lane
-constexpr uint32_t kSgCandCap = 1024;                // entry candidates per record
-// payload bytes per lane for the CRC: 49 words, an odd word stride between lanes, so the data reads
-// of a 32-lane group hit 32 different banks (48 words put every other lane on the same bank)
-constexpr uint32_t kSgQ = 196;
-constexpr uint32_t kCstStageLane = 128;              // consts [128, 192): x^(8 * kSgQ * (63 - l)),
-                                                     // [192, 256): x^(8 * (kSgQ * (63 - l) + 96))
-constexpr uint32_t kSgRegion = (kWStageStride + 2u * kSgCandCap + 64u * 16u + 32u + 15u) & ~15u;
-static_assert(kSgQ * 64 >= kWStage && kSgQ % 4 == 0 && (kSgQ / 4) % 2 == 1, "lane CRC slices");
-
-// bit 7 of every byte of x that is zero, exactly (no borrow from a lower byte)
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t x) {
-  return ~(((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x | 0x7f7f7f7fu);
-}
-
-// word y of the payload [a, b) (stage offsets): bytes outside zeroed, bytes [a, a + 4) inverted
-__device__ __forceinline__ uint32_t sg_mask_word(uint32_t w, uint32_t y, uint32_t a, uint32_t b) {
-  auto below = [](uint32_t x, uint32_t y_) {  // bytes of the word at y_ below x
-    return x <= y_ ? 0u : (x - y_ >= 4u ? 0xffffffffu : (1u << ((x - y_) << 3)) - 1u);
-  };
-  const uint32_t ba = below(a, y), keep = below(b, y) & ~ba, inv = below(a + 4u, y) & ~ba & keep;
-  return (w & keep) ^ inv;
-}
-
-// masked CRC-32C of the payload at stage [a, b) equals `stored` (L = b - a >= 256). Each lane's
-// 49 words run as two independent chains (its first 25 words and its last 24: twice the LDS
-// round trips in flight), placed by x^(8 (196 (63 - l) + 96)) and x^(8 * 196 (63 - l)).
-__device__ __forceinline__ bool sg_payload_crc(const uint8_t* l, uint32_t a, uint32_t b, uint32_t stored,
-                                               const LdsTab<1>& T, uint32_t Kl, uint32_t KlA, uint32_t lane) {
-  const uint32_t* W = reinterpret_cast<const uint32_t*>(l);
-  const uint32_t bw = (b + 3u) & ~3u, z = bw - b;
-  const uint32_t back = kSgQ * (63u - lane);  // bytes between this lane's words and bw
-  const uint32_t a4 = a & ~3u;
-  uint32_t S = 0;
-  if (bw > back + a4) {  // some payload byte in this lane's words
-    const uint32_t x1 = bw - back;
-    // words below a4 (masked to zero: a zero state stays zero) may precede the payload: a framed
-    // payload starts at stage offset >= 12, so x1 - 196 >= 0 unless this lane holds the start;
-    // there the chains begin at the first pair holding a4 - 4 or later
-    // (signed: the slice of the lane holding the payload start may begin before the stage; only
-    // words at or above a4 - 4 >= 8 are read)
-    const int32_t yA = (int32_t)x1 - (int32_t)kSgQ, yB = (int32_t)x1 - 96, ia4 = (int32_t)a4;
-    auto word = [&](int32_t y) {
-      const uint32_t w = W[y >> 2];
-      return ((uint32_t)y < a + 4u || (uint32_t)y + 4u > b) ? sg_mask_word(w, (uint32_t)y, a, b) : w;
-    };
-    uint32_t SA = yA + 4 > ia4 ? T.step4(word(yA)) : 0u, SB = 0u;  // chain A: 1 + 12 pairs
-#pragma unroll 2
-    for (int32_t k = 0; k < 12; ++k) {
-      const int32_t ya = yA + 4 + 8 * k, yb = yB + 8 * k;
-      if (ya + 8 > ia4) SA = T.step8(SA ^ word(ya), word(ya + 4));
-      if (yb + 8 > ia4) SB = T.step8(SB ^ word(yb), word(yb + 4));
-    }
-    S = gf_mul(SA, KlA) ^ gf_mul(SB, Kl);
-  }
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) S ^= (uint32_t)__shfl_xor((int)S, m, 64);
-  const uint32_t um = stored - kCrcMaskDelta;
-  uint32_t v = ~((um << 15) | (um >> 17));  // ~crc_mask^-1(stored) = U(~0, payload) un-inverted
-  for (uint32_t k = 0; k < z; ++k) v = (v >> 8) ^ T(0u, v & 0xffu);
-  return v == S;
-}
-
-
-// count_packed over the LDS stage, one aligned 16-byte block per step (one ds_read_b128) and the
-// block's 16 continuation bits at once: terminators = popcount, the run of continuation bytes
-// carried across blocks checked at the first terminator, runs of >= 10 after a terminator found by
-// a 10-fold AND of shifts. Same verdicts as count_packed (a varint of > 10 bytes, or a chunk not
-// ending on a terminator, bails), without its byte-serial dependency chain.
-__device__ __forceinline__ bool count_packed16(const FastSrc& s, uint32_t o, uint32_t e, uint32_t& cnt) {
-  uint32_t run = 0, terms = 0;
-  bool bad = false;
-  const uint32_t a0 = s.p + o, a1 = s.p + e;
-  for (uint32_t q = a0 & ~15u; q < a1; q += 16u) {
-    const uint4 blk = *reinterpret_cast<const uint4*>(s.l + q);
-    const uint32_t lo = a0 > q ? a0 - q : 0u, hi = a1 - q < 16u ? a1 - q : 16u;  // valid bytes [lo, hi)
-    packed_block(blk, lo, hi, run, terms, bad);
-  }
-  if (bad || (e > o && run)) return false;  // the last varint runs past the chunk
-  cnt = terms;
-  return true;
-}
-
-template <bool COMPAT>
-__global__ __launch_bounds__(kWaveBlock, 2) void k_stage_count(DevBatch B, DevSchema sc, DevOut o,
-                                                               const uint32_t* __restrict__ crc_tab,
-                                                               const uint32_t* __restrict__ consts) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-  const uint32_t nbig = o.info[kInfoBig];
-  if (blockIdx.x * kWavesPerBlock >= nbig) return;  // block-uniform
-  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  uint32_t* tab = lds;  // [8][256] slice-by-8
-  uint32_t* kht = lds + 2048;
-  uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
-  uint8_t* region = reinterpret_cast<uint8_t*>(krec + sc.n_keys * kKrWords) + wib * kSgRegion;
-  uint8_t* stage = region;
-  uint16_t* cand = reinterpret_cast<uint16_t*>(region + kWStageStride);
-  uint32_t* d_ord = reinterpret_cast<uint32_t*>(cand + kSgCandCap);
-  uint32_t* d_cw = d_ord + 64;
-  uint2* d_lv = reinterpret_cast<uint2*>(d_cw + 64);
-  uint32_t* seen = reinterpret_cast<uint32_t*>(d_lv + 64);
-  for (uint32_t i = threadIdx.x; i < 2048u; i += kWaveBlock) tab[i] = crc_tab[2048 + i];
-  for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kWaveBlock) kht[i] = sc.ht[i];
-  for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kWaveBlock) krec[i] = sc.krec[i];
-  __syncthreads();
-  const LdsTab<1> T{tab, 0};
-  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
-  const uint32_t S = sc.n_slots;
-  const uint32_t Kl = consts[kCstStageLane + lane], KlA = consts[kCstStageLane + 64 + lane];
-  const uint32_t spec_k = (sc.spec && lane < S) ? sc.spec[lane] : 0u;
-  const bool framed = !(B.flags & kFlagPayloadOnly), do_crc = framed && !(B.flags & kFlagNoCrc);
-  const uint32_t* W = reinterpret_cast<const uint32_t*>(stage);
-
-  const uint32_t stride = gridDim.x * kWavesPerBlock;
-  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
-  if (i >= nbig) return;  // wave-uniform (no block barrier below)
-  // three-stage record queue, as role_stage_gather: the next record's bytes in registers while this
-  // one is counted from the stage
-  RecPipe q;
-  q.r1 = o.big_list[i];
-  q.s1 = B.start[q.r1];
-  q.e1 = B.end[q.r1];
-  Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
-  q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
-  q.s2v = B.start[vgpr_launder(q.r2)];
-  q.e2v = B.end[vgpr_launder(q.r2)];
-  q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
-  for (; i < nbig; i += stride) {
-    PHASE_MARK(t0);
-    const uint32_t r = q.r1;
-    const RecView v = rec_view_se(B, q.s1, q.e1);
-    const uint64_t lo16 = v.st & ~15ull;
-    pref_store(pf, stage, lo16, v.e, lane);
-    if (lane < 64u) {
-      d_ord[lane] = 0u;
-      if (lane < 8u) seen[lane] = 0u;
-    }
-    wave_lds_sync();
-    q.r1 = q.r2;
-    q.s1 = rfl64(q.s2v);
-    q.e1 = rfl64(q.e2v);
-    q.r2 = rfl32(q.r3v);
-    q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
-    if (i + stride < nbig) pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.e1 < B.nbytes ? q.e1 : B.nbytes, lane);
-    q.s2v = B.start[vgpr_launder(q.r2)];
-    q.e2v = B.end[vgpr_launder(q.r2)];
-    PHASE_MARK(t1);
-    PHASE_ADD(0, t0, t1);
-
-#ifdef TFRG_SG_ONLY_STAGE
-    if (lane == 0) o.verdict[r] = (uint8_t)W[lane];
-    wave_lds_sync();
-    continue;
-#endif
-    // ---- framing verdicts (frame_verdicts' conditions)
-    uint32_t verdict = v.verdict;
-    const uint32_t so = (uint32_t)(v.st - lo16), pa = (uint32_t)(v.p0 - lo16), L = (uint32_t)v.L;
-    const uint64_t D = v.e - v.st;
-    if (framed && D >= 8) {
-      const uint32_t lw0 = lds_u32u(stage, so), lw1 = lds_u32u(stage, so + 4u);
-      if ((((uint64_t)lw1 << 32) | lw0) == v.en - v.st - 16) verdict |= TFRG_V_LEN_MATCH;
-      if (do_crc && D >= 12) {
-        const uint32_t c = ~T.step4(T.step4(0xffffffffu ^ lw0) ^ lw1);
-        if (crc_mask(c) == lds_u32u(stage, so + 8u)) verdict |= TFRG_V_LEN_CRC;
-      }
-      if (do_crc && D >= 16) {
-        const uint32_t stored = lds_u32u(stage, pa + L);
-        const bool okc = L >= 256u ? sg_payload_crc(stage, pa, pa + L, stored, T, Kl, KlA, lane)
-                                   : crc_mask(crc_lds8<1>(stage, pa, pa + L, T)) == stored;
-        if (okc) verdict |= TFRG_V_DATA_CRC;
-      }
-    }
-
-    PHASE_MARK(t2);
-    PHASE_ADD(1, t1, t2);
-#ifdef TFRG_SG_NO_PARSE
-    if (lane == 0) o.verdict[r] = (uint8_t)verdict;
-    wave_lds_sync();
-    continue;
-#endif
-    // ---- entry-parallel canonical walk
-    const FastSrc fs{stage, pa, L, v.p0};
-    uint32_t fn, fo, fl;
-    bool good = hdr2(fs, 0, L, fn, fo, fl) & (fn == 1u) & (fo + fl == L);
-    const uint32_t fe = fo + fl;
-    // entry-start candidates of the body, 256 bytes per step (lane j: aligned word j, so the reads
-    // are bank-conflict-free): position p (stage offset) holding 0x0a, then a 1-byte length and
-    // 0x0a, or a 2-byte length and 0x0a; numbered across the wave in position order
-    const uint32_t ba = pa + fo, be = pa + fe;
-    uint32_t total = 0;
-    if (good) {
-      const uint64_t lt = (1ull << lane) - 1ull;
-      for (uint32_t row = ba & ~15u; row < be; row += 1024u) {  // (wave-uniform)
-        const uint32_t y = row + 16u * lane;
-        uint4 blk = make_uint4(0, 0, 0, 0);
-        if (y < be) blk = *reinterpret_cast<const uint4*>(stage + y);
-        uint32_t nxt = (uint32_t)__shfl_down((int)blk.x, 1, 64);  // the next block's first word
-        if (lane == 63u && y + 16u < be) nxt = W[(y + 16u) >> 2];
-        const uint32_t ws[5] = {blk.x, blk.y, blk.z, blk.w, nxt};
-        uint32_t c16 = 0;  // candidate bits: bit 4k + j = position y + 4k + j
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const uint32_t w = ws[k], wn = ws[k + 1];
-          const uint32_t w1 = __builtin_amdgcn_alignbyte(wn, w, 1u), w2 = __builtin_amdgcn_alignbyte(wn, w, 2u);
-          const uint32_t w3 = __builtin_amdgcn_alignbyte(wn, w, 3u);
-          const uint32_t e0 = zero_bytes(w ^ 0x0a0a0a0au), e2 = zero_bytes(w2 ^ 0x0a0a0a0au);
-          const uint32_t e3 = zero_bytes(w3 ^ 0x0a0a0a0au);
-          const uint32_t h1 = w1 & 0x80808080u, h2 = w2 & 0x80808080u;
-          const uint32_t c = (e0 & ((~h1 & e2) | (h1 & ~h2 & e3))) >> 7;  // bit 8 j: position 4k + j
-          c16 |= ((c | (c >> 7) | (c >> 14) | (c >> 21)) & 0xfu) << (4 * k);
-        }
-        // positions inside the body
-        const uint32_t lo = ba > y ? (ba - y < 16u ? ba - y : 16u) : 0u, hi = be > y ? (be - y < 16u ? be - y : 16u) : 0u;
-        c16 &= ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-        const uint32_t nc = (uint32_t)__popc(c16);
-        const uint64_t b0 = __ballot(nc & 1u), b1 = __ballot(nc & 2u), b2 = __ballot(nc & 4u);
-        const uint64_t b3 = __ballot(nc & 8u), b4 = __ballot(nc & 16u);
-        uint32_t at = total + (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) +
-                      4u * (uint32_t)__popcll(b2 & lt) + 8u * (uint32_t)__popcll(b3 & lt) +
-                      16u * (uint32_t)__popcll(b4 & lt);
-        while (c16) {
-          if (at < kSgCandCap) cand[at] = (uint16_t)(y + (uint32_t)__builtin_ctz(c16));
-          ++at;
-          c16 &= c16 - 1u;
-        }
-        total += (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2) +
-                 8u * (uint32_t)__popcll(b3) + 16u * (uint32_t)__popcll(b4);
-      }
-    }
-    good &= total <= kSgCandCap;
-    wave_lds_sync();
-#ifdef TFRG_SG_SCAN_ONLY
-    if (lane == 0) o.verdict[r] = (uint8_t)(verdict + total);
-    wave_lds_sync();
-    continue;
-#endif
-    PHASE_MARK(t3);
-    PHASE_ADD(3, t2, t3);
-    uint32_t chain = fo, rank0 = 0;  // payload offset the next entry must start at; entries so far
-    for (uint32_t w0 = 0; good && w0 < total; w0 += 64u) {  // (wave-uniform)
-      const uint32_t ci = w0 + lane;
-      const bool has = ci < total;
-      const uint32_t qp = has ? (uint32_t)cand[ci] - pa : fo;  // payload offset of the candidate
-      uint32_t en, eo, el, kn, ko, kl, vn, vo, vl, kind, lo, ll;
-      bool pat = has & hdr2(fs, qp, fe, en, eo, el) & (en == 1u);
-      const uint32_t ee = eo + el;
-      pat &= hdr2(fs, eo, ee, kn, ko, kl) & (kn == 1u);
-      pat &= hdr2(fs, ko + kl, ee, vn, vo, vl) & (vn == 2u) & (vo + vl == ee);
-      pat &= hdr2(fs, vo, ee, kind, lo, ll) & (lo + ll == ee) & (kind - 1u < 3u);
-      // the surviving candidates must chain: each starts where the previous one ends
-      const uint64_t pm = __ballot(pat);
-      const uint64_t below = pm & ((1ull << lane) - 1ull);
-      const int pl = below ? 63 - __builtin_clzll(below) : 0;
-      const uint32_t pend = (uint32_t)__shfl((int)ee, pl, 64);
-      const uint32_t want = below ? pend : chain;
-      good &= !__ballot(pat && qp != want);
-      if (!good) break;
-      const uint32_t rank = rank0 + (uint32_t)__popcll(below) + 1u;
-      bool eok = true;
-      if (pat) {
-        const int kid = fast_lookup(fs, K, ko, kl);
-        uint32_t cnt = 0, nch = 0, c0o = 0, c0l = 0, c0w = 0;
-        const uint32_t le = lo + ll;
-        for (uint32_t g = lo; eok && g < le;) {
-          uint32_t cf, co, cl;
-          eok = hdr2(fs, g, le, cf, co, cl) & (cf == 1u);
-          g = co + cl;
-          if (kind == TFRG_KIND_BYTES) {
-            ++cnt;
-          } else if (kind == TFRG_KIND_FLOAT) {
-            eok &= (cl & 3u) == 0u;
-            cnt += cl >> 2;
-          } else if (cl <= 4u) {
-            const uint32_t m = bytes_mask(cl);
-            const uint32_t wv = fs.u32(co) & m;
-            const uint32_t tm = ~wv & 0x80808080u & m;
-            eok &= cl == 0u || ((tm >> ((cl << 3) - 1u)) & 1u);
-            cnt += __popc(tm);
-            if (nch == 0) c0w = wv;
-          } else {
-            uint32_t kk = 0;
-#ifndef TFRG_SG_NO_COUNT
-            eok &= count_packed16(fs, co, co + cl, kk);
-#else
-            kk = cl >> 2;
-#endif
-            cnt += kk;
-          }
-          if (nch == 0) {
-            c0o = co;
-            c0l = cl;
-          }
-          ++nch;
-        }
-        eok &= kid >= 0;
-        int slot = -1;
-        if (eok) {
-          slot = (int)K.rec[(uint32_t)kid * kKrWords + kKrSlot1 + kind - 1u];
-          const uint32_t bit = 1u << ((uint32_t)kid & 31u);
-          const uint32_t old = atomicOr(&seen[(uint32_t)kid >> 5], bit);  // a duplicate key bails
-          eok &= !(old & bit) & (slot >= 0) & (rank < 65534u);
-        }
-        if (eok) {
-          uint2 lv = make_uint2(lo, ll);
-          uint32_t cw = cnt;
-          if (cnt == 1u && nch == 1u) {
-            if (kind == TFRG_KIND_BYTES) {
-              lv = make_uint2((uint32_t)(fs.base + c0o), c0l);
-              cw = 1u | kCountInline;
-            } else if (kind == TFRG_KIND_FLOAT) {
-              lv = make_uint2(fs.u32(c0o), 0u);
-              cw = 1u | kCountInline;
-            } else if (c0l <= 4u) {
-              lv = make_uint2(vgroups(c0w, 0xffffffffu), 0u);
-              cw = 1u | kCountInline;
-            }
-          }
-          d_ord[slot] = rank;
-          d_cw[slot] = cw;
-          d_lv[slot] = lv;
-        }
-      }
-      good &= !__ballot(pat && !eok);
-      if (pm) chain = __builtin_amdgcn_readlane(ee, 63 - __builtin_clzll(pm));
-      rank0 += (uint32_t)__popcll(pm);
-    }
-    good &= chain == fe;
-    wave_lds_sync();
-    PHASE_MARK(t4);
-    PHASE_ADD(4, t3, t4);
-
-    // ---- results
-    if (!good || !strict_pass(B, verdict, true)) {  // the exact walker (k_tail_count role 1)
-      if (lane == 0) {
-        const uint32_t si = atomicAdd(&o.info[kInfoSlow], 1u);
-        o.slow_list[si] = r;
-        o.verdict[r] = (uint8_t)kVerdictPending;
-      }
-      if (spec_k) atomicAdd(&o.irr[lane], 1u);
-    } else {
-      if (lane == 0) {
-        o.status[r] = TFRG_OK;
-        o.verdict[r] = (uint8_t)verdict;
-      }
-      if (lane < S) {
-        const uint32_t ov = d_ord[lane];
-        const uint32_t cw = ov ? d_cw[lane] : 0u;
-        const size_t at = (size_t)lane * B.n + r;
-        o.order[at] = (uint16_t)ov;
-        o.count[at] = cw;
-        if (ov) {
-          const uint2 lv = d_lv[lane];
-          if (spec_k && (cw & kCountInline)) put_inline(o, spec_k & 3u, lv, (uint64_t)B.n * ((spec_k >> 2) - 1u) + r);
-          else o.loc[at] = lv;
-        }
-#ifndef TFRG_SG_NO_TSUM
-        if (cw & ~kCountInline) atomicAdd(&o.tsum[(size_t)lane * o.tile_stride + (r >> kTileShift)], cw & ~kCountInline);
-#endif
-        if (spec_k && cw != (1u | kCountInline)) atomicAdd(&o.irr[lane], 1u);
-      }
-    }
-    wave_lds_sync();  // (the stage and the dict are rewritten by the next record)
-    PHASE_MARK(t5);
-    PHASE_ADD(6, t4, t5);
-    PHASE_ADD(7, t0, t5);
-  }
-}
 
 // ------------------------------------------------------------------------------------------------
 // Row-split scan, second level: the tile sums of every slot in chunks of 4096 tiles (1 M records),
@@ -3391,7 +2389,11 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
     const uint64_t r1 = r0 + (1ull << (kSpineChunkShift + kTileShift)) < n ? r0 + (1ull << (kSpineChunkShift + kTileShift)) : n;
     for (uint64_t r = r0 + threadIdx.x; r < r1; r += kSpineBlock) {
       const size_t at = (size_t)slot * n + r;
-      if (o.count[at] != (1u | kCountInline)) continue;
+      if (o.lmask && !((o.lmask[r >> 6] >> (r & 63u)) & 1ull)) {
+        o.count[at] = 1u | kCountInline;  // a k_tpl_lane record (placed, its count word not written)
+      } else if (o.count[at] != (1u | kCountInline)) {
+        continue;
+      }
       const uint64_t p = sb + r;
       uint2 lv = make_uint2(0, 0);
       if ((sw & 3u) == TFRG_KIND_INT64) {
@@ -3491,37 +2493,31 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
 // ------------------------------------------------------------------------------------------------
 // Gather: decode the (validated) list message of every present slot into its column.
 // ------------------------------------------------------------------------------------------------
+// list_values into the value columns from element dst on (stores past a capacity dropped)
+struct ColOut {
+  const DevOut& o;
+  uint64_t base;  // absolute payload start (bytes views)
+  uint64_t dst;
+  __device__ __forceinline__ void bytes(int64_t off, int64_t len) {
+    if (dst < o.cap_b) {
+      o.b_off[dst] = (uint32_t)(base + (uint64_t)off);
+      o.b_len[dst] = (uint32_t)len;
+    }
+    ++dst;
+  }
+  __device__ __forceinline__ void f32(uint32_t bits) {
+    if (dst < o.cap_f32) o.f32[dst] = bits;
+    ++dst;
+  }
+  __device__ __forceinline__ void i64(int64_t v) {
+    if (dst < o.cap_i64) o.i64[dst] = v;
+    ++dst;
+  }
+};
 template <bool COMPAT, class S>
 __device__ void list_gather(S& s, const DevOut& o, int kind, int64_t lo, int64_t ll, uint64_t dst) {
-  const int64_t end = lo + ll;
-  int64_t pos = lo, aux = 0;
-  Fld f;
-  while (pos < end) {
-    rd_field<COMPAT>(s, pos, end, f, aux);
-    if (f.fn != 1) continue;
-    if (kind == TFRG_KIND_BYTES) {
-      if (dst < o.cap_b) {
-        o.b_off[dst] = (uint32_t)(s.p0 + (uint64_t)f.off);
-        o.b_len[dst] = (uint32_t)f.len;
-      }
-      ++dst;
-    } else if (kind == TFRG_KIND_FLOAT) {
-      const int64_t m = f.wt == 2 ? (f.len >> 2) : 1;
-      for (int64_t i = 0; i < m; ++i) {
-        if (dst < o.cap_f32) o.f32[dst] = s.u32(f.off + 4 * i);
-        ++dst;
-      }
-    } else {
-      int64_t p = f.off;
-      const int64_t e = f.off + f.len;
-      while (p < e) {
-        int64_t val = 0;
-        rd_varint<COMPAT>(s, p, val);
-        if (dst < o.cap_i64) o.i64[dst] = val;
-        ++dst;
-      }
-    }
-  }
+  ColOut out{o, s.p0, dst};
+  list_values<COMPAT>(s, kind, lo, ll, out);
 }
 
 // one int64 varint at `pos` of a validated packed chunk ending at `e` (fast path): <= 4 bytes from
@@ -3598,10 +2594,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
                                                             uint32_t n_tiles) {
   // slots per scan group (one barrier each): 2 beside 4 tiles per workgroup, 8 with one tile (small
   // batches and wide schemas: fewer barriers between the loads, same registers)
-#ifndef TFRG_DG1
-#define TFRG_DG1 8
-#endif
-  constexpr uint32_t kDG = kDT == 1 ? (uint32_t)TFRG_DG1 : 2u;
+  constexpr uint32_t kDG = kDT == 1 ? 8u : 2u;
   __shared__ uint32_t s_w[2][kDT * kDG][4];  // wave totals, double-buffered across slot groups
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t S = sc.n_slots;
@@ -4084,15 +3077,8 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
-#ifndef TFRG_FG
-#define TFRG_FG 8
-#endif
-  constexpr int kFG = TFRG_FG;
-#ifdef TFRG_DIAG_NOFLOAT  // diagnostic build (timing only, values missing): no float copies
-  uint64_t m = 0;
-#else
+  constexpr int kFG = 8;
   uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
-#endif
   while (m) {
     uint32_t fb[kFG], fn[kFG];
     uint64_t fd[kFG];
@@ -4120,15 +3106,8 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   // canonical packed int64 lists: balanced over the whole wave
   const bool iv = packed && kind == TFRG_KIND_INT64 && bl > 0u && fs.l[fs.p + bo + bl - 1u] < 0x80u;
   fail |= packed && kind == TFRG_KIND_INT64 && !iv;
-#ifndef TFRG_INT64_RING
-#define TFRG_INT64_RING 1
-#endif
-#ifdef TFRG_DIAG_NOINT64  // diagnostic build (timing only, values missing): no int64 decode
-  int rr = 1;
-#else
-  int rr = TFRG_INT64_RING ? int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring) : -1;
+  int rr = int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring);
   if (rr < 0) rr = int64_balanced<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane) ? 1 : 0;
-#endif
   if (!rr) fail |= iv;
   PHASE_MARK(g1);
   PHASE_ADD(11, gf, g1);
@@ -4143,14 +3122,8 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   PHASE_ADD(12, g1, g2);
 }
 
-// Medium records, one wave each, staged in LDS. TFRG_GATHER_PREF = 1 (default) loads the next
-// record's bytes into registers while this one is gathered (48 VGPRs live across the gather);
-// 0 stages each record when it starts: 4 instead of 3 waves' registers per SIMD, but the 12 KiB
-// stages cap the CU at 12 waves anyway (C3 gather 1.654 vs 1.636 ms; a 9 KiB stage for 16 waves
-// sent C3's larger records to the HBM path: 1.918 ms).
-#ifndef TFRG_GATHER_PREF
-#define TFRG_GATHER_PREF 1
-#endif
+// Medium records, one wave each, staged in LDS. The next record's bytes are loaded into registers
+// while this one is gathered (48 VGPRs live across the gather).
 template <bool COMPAT>
 __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage,
                                   uint16_t* ring) {
@@ -4164,9 +3137,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
   q.s1 = B.start[q.r1];
   q.e1 = B.end[q.r1];
   q.t1 = i < nbig ? o.status[q.r1] : -1;
-#if TFRG_GATHER_PREF
   Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
-#endif
   q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
   q.s2v = B.start[vgpr_launder(q.r2)];
   q.e2v = B.end[vgpr_launder(q.r2)];
@@ -4197,14 +3168,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     const bool ok = q.t1 == TFRG_OK;
     const RecView v = rec_view_se(B, q.s1, q.e1);
     const uint64_t lo16 = v.st & ~15ull;
-#if TFRG_GATHER_PREF
     if (ok) pref_store(pf, stage, lo16, v.e, lane);
-#else
-    if (ok) {  // this record's bytes: all loads in flight, then the stores (registers live only here)
-      const Pref cur = pref_load_v(B.bytes, lo16, v.e, lane);
-      pref_store(cur, stage, lo16, v.e, lane);
-    }
-#endif
     wave_lds_sync();
     // slot metadata of this record (loaded during the previous one)
     const uint32_t c = c_n, kind = kind_l;
@@ -4217,9 +3181,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     q.t1 = i + stride < nbig ? (int32_t)rfl32((uint32_t)q.t2v) : -1;
     q.r2 = rfl32(q.r3v);
     q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
-#if TFRG_GATHER_PREF
     pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
-#endif
     q.s2v = B.start[vgpr_launder(q.r2)];
     q.e2v = B.end[vgpr_launder(q.r2)];
     q.t2v = o.status[vgpr_launder(q.r2)];
@@ -4272,12 +3234,9 @@ __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchem
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (slice-by-8: 8 KiB per copy)
 
-#ifndef TFRG_LANE_LDS_BUDGET
-#define TFRG_LANE_LDS_BUDGET (64 * 1024)
-#endif
-constexpr size_t kLaneLdsBudget = TFRG_LANE_LDS_BUDGET;  // lane kernels (occupancy): likewise
+constexpr size_t kLaneLdsBudget = 64 * 1024; // lane kernels (occupancy): likewise
 
-const char* const kStageNames[kNumStages] = {"k_lane_count",  "k_stage_count", "k_body_count", "k_tail_count", "k_spine",
+const char* const kStageNames[kNumStages] = {"k_tpl_lane",    "k_lane_count",  "k_body_count", "k_tail_count", "k_spine",
                                              "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -4292,20 +3251,56 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const uint32_t n_tiles = (b.n + kTileRecs - 1) / kTileRecs;
   const size_t dict_lane = S * kLaneCountBlock * 4 + r16(S * kLaneCountBlock * 2);  // cnt u32 + ord u16 per lane
   const size_t tab_lds = 256ull * kLaneSlice * kLaneRep * 4;
-  const size_t stage_lds = (size_t)kStageStride * kLaneBufs * (kLaneCountBlock / 64);
+  const size_t stage_lds = (size_t)kStageStride * (kLaneCountBlock / 64);
   const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;
   const size_t keys_lds = fast_ok ? (((size_t)sc.ht_mask + 4) / 4 * 4 + (size_t)sc.n_keys * kKrWords) * 4 : 0;
-  const size_t tpl_lds = fast_ok && !TFRG_TPL_SMEM ? (size_t)sc.n_tpl * kTplWords * 4 : 0;  // (TplRef)
   // (MODE 0 only) spec words + their targets
   const size_t spec_lds = fast_ok && sc.spec ? ((S + 7) & ~(size_t)7) * 4 + S * kSpecTgtWords * 4 : 0;
-  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + tpl_lds + spec_lds;
+  const size_t lane_lds = tab_lds + dict_lane + stage_lds + keys_lds + spec_lds;
   // speculative placement only with the per-lane LDS dict (MODE 0); the later kernels see the same
   DevSchema scx = sc;
   if (lane_lds > kLaneLdsBudget || !fast_ok) scx.spec = nullptr;
   const uint32_t wave_stage = cfg.wave_stage < kWStage ? cfg.wave_stage : kWStage;
-  // staged large records counted by k_stage_count (else the lane kernel walks them from HBM)
-  const uint32_t sg = cfg.stage_count && fast_ok && S <= kSgMaxSlots ? 1u : 0u;
-
+  // record-shape templates first (k_tpl_lane, tfrg_tpl.hip): framed records with CRC verdicts, a
+  // schema of <= kLeanMaxSlots slots; k_lane_count then takes only the records it left
+  const bool lean = cfg.lean && sc.n_tpl && fast_ok && S <= kLeanMaxSlots && o.lmask && o.rlist &&
+                    (sc.tpl_w == 16 || sc.tpl_w == 32 || sc.tpl_w == 64) &&
+                    !(b.flags & (kFlagPayloadOnly | kFlagNoCrc)) && b.nbytes < 0xffffff00ull;
+  DevOut ox = o;
+  if (!lean) {
+    ox.lmask = nullptr;
+    ox.rlist = nullptr;
+  }
+  mark(kStageTplLane);
+  if (lean) {
+    LeanArgs a{};
+    a.n_tpl = sc.n_tpl;
+    a.lane_max = cfg.lane_max;
+    a.tsum = o.tsum;
+    const uint64_t n = b.n;
+    for (uint32_t k = 0; k < S; ++k) {
+      LeanTgt& t = a.tg[k];
+      t.ord = o.order + k * n;
+      t.cnt = o.count + k * n;
+      t.loc = o.loc + k * n;
+      t.rs = o.rs + k * (n + 1);
+      t.tsum = k * o.tile_stride;
+      const uint32_t sw = scx.spec && cfg.spec_h ? cfg.spec_h[k] : 0u;
+      if (sw) {  // as spec_target: column rows n * (rank - 1) + r, r below the capacity
+        const uint32_t kind = sw & 3u;
+        const uint64_t base = n * ((sw >> 2) - 1u);
+        const uint64_t cap = kind == TFRG_KIND_INT64 ? o.cap_i64 : kind == TFRG_KIND_FLOAT ? o.cap_f32 : o.cap_b;
+        t.lim = cap > base ? (uint32_t)std::min<uint64_t>(cap - base, n) : 0u;
+        t.kind = kind;
+        if (kind == TFRG_KIND_INT64) t.v1 = o.i64 + base;
+        else if (kind == TFRG_KIND_FLOAT) t.v1 = o.f32 + base;
+        else t.v1 = o.b_off + base;
+        t.v2 = o.b_len + base;
+      }
+    }
+    const hipError_t e = launch_tpl_lane(b, ox, a, sc.tpl, sc.tpl_w, d_tab, cfg.num_cus, st);
+    if (e != hipSuccess) return e;
+  }
   mark(kStageLaneCount);
   // one round of resident workgroups (a second, partial round would idle most CUs at the tail)
   auto resident_grid = [&](const void* fn, size_t lds, bool cap = true) {
@@ -4319,32 +3314,22 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
-                       dim3(kLaneCountBlock), lane_lds - tab_lds, st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
+                       dim3(kLaneCountBlock), lane_lds - tab_lds, st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
   } else if (S <= 64) {
-    const size_t lds = stage_lds + keys_lds + (kLaneCountBlock / 64) * 64 * 4 + tpl_lds;  // (+ the static tables)
+    const size_t lds = stage_lds + keys_lds + (kLaneCountBlock / 64) * 64 * 4;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
-                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
+                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
   } else {
-    const size_t lds = stage_lds + keys_lds + tpl_lds;  // (+ the static tables)
+    const size_t lds = stage_lds + keys_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
-                       st, b, scx, o, d_tab, cfg.lane_max, wave_stage, sg);
-  }
-  mark(kStageStageCount);
-  if (sg) {  // one round of resident workgroups over the staged large records
-    const size_t lds = 2048 * 4 + keys_lds + (size_t)kSgRegion * kWavesPerBlock;
-    const void* fn = reinterpret_cast<const void*>(&k_stage_count<COMPAT>);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
-    hipLaunchKernelGGL((k_stage_count<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, d_tab, d_consts);
+                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
   }
   mark(kStageBodyCount);
   if (cfg.body_count && lane_lds > kLaneLdsBudget) {  // deferred bodies (lane modes 1 and 2 only)
     const uint32_t g = 8u * (uint32_t)cfg.num_cus;
-    hipLaunchKernelGGL(k_body_count, dim3(g), dim3(kBodyBlock), 0, st, b, o);
+    hipLaunchKernelGGL(k_body_count, dim3(g), dim3(kBodyBlock), 0, st, b, ox);
   }
   mark(kStageTailCount);
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
@@ -4361,15 +3346,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       per_cu = 1;
     const uint32_t g = (uint32_t)(per_cu * cfg.num_cus);
     if (gord)
-      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, o, d_tab, d_consts,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab, d_consts,
                          cfg.lane_max);
     else
-      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, o, d_tab,
+      hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab,
                          d_consts, cfg.lane_max);
   }
   mark(kStageSpine);
   if (S > 0)
-    hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, o, sc.slot_kind, (uint32_t)S, n_tiles,
+    hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, ox, sc.slot_kind, (uint32_t)S, n_tiles,
                        scx.spec, b.n);
   mark(kStageDownGather);
   if (S > 0) {
@@ -4378,10 +3363,10 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus) {
       const uint32_t ng = (n_tiles + 3) / 4;
       hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3(ng < resident ? ng : resident), dim3(kLaneBlock), 0, st, b,
-                         scx, o, cfg.lane_max, n_tiles);
+                         scx, ox, cfg.lane_max, n_tiles);
     } else {
       hipLaunchKernelGGL((k_down_gather<COMPAT, 1>), dim3(n_tiles < resident ? n_tiles : resident), dim3(kLaneBlock),
-                         0, st, b, scx, o, cfg.lane_max, n_tiles);
+                         0, st, b, scx, ox, cfg.lane_max, n_tiles);
     }
   }
   mark(kStageTailGather);
@@ -4392,7 +3377,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
-    hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, o, cfg.lane_max);
+    hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, ox, cfg.lane_max);
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)
   return hipGetLastError();

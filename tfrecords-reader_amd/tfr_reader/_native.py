@@ -39,6 +39,25 @@ class TfrgInfo(C.Structure):
         ("kind_totals", C.c_uint64 * 4),
         ("nbytes", C.c_uint64),
         ("bytes_data_len", C.c_uint64),
+        ("tpl_groups_missed", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class TfrgHostRecord(C.Structure):
+    _fields_ = [
+        ("status", C.c_int32),
+        ("n_entries", C.c_uint32),
+        ("aux", C.c_int64),
+        ("key_off", u32p),
+        ("key_len", u32p),
+        ("kind", u8p),
+        ("val_off", u32p),
+        ("val_cnt", u32p),
+        ("i64", i64p),
+        ("f32", u32p),
+        ("b_off", u32p),
+        ("b_len", u32p),
     ]
 
 
@@ -83,10 +102,16 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_ctx_set_lane_max": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_wave_stage": (C.c_int, [C.c_void_p, C.c_uint32]),
     "tfrg_ctx_set_record_bound": (C.c_int, [C.c_void_p, C.c_uint64]),
-    "tfrg_ctx_set_stage_count": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_learn_templates": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
                                        C.c_uint32]),
+    "tfrg_host_ctx_create": (C.c_int, [C.c_void_p]),
+    "tfrg_host_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "tfrg_host_decode": (C.c_int, [C.c_void_p, C.c_char_p, C.c_uint64, C.c_uint32, C.POINTER(TfrgHostRecord)]),
     "tfrg_template_count": (C.c_int, [C.c_void_p]),
+    "tfrg_template_words": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    "tfrg_learn_templates_host": (C.c_int, [C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32,
+                                            C.c_uint32, C.c_void_p, C.c_uint64, C.c_void_p]),
     "tfrg_ctx_set_templates": (C.c_int, [C.c_void_p, C.c_int]),
     "tfrg_stream_read": (C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]),
     "tfrg_device_count": (C.c_int, []),

@@ -1,4 +1,5 @@
-"""``example_from_bytes`` (reference: cython/decoder.pyx:107) on the GPU decoder.
+"""``example_from_bytes`` (reference: cython/decoder.pyx:107): libtfrg's host decode of the record
+(tfr_reader/host.py), or the GPU for payloads above ``host.HOST_MAX_BYTES``.
 
 Returns an object graph with the reference's shape: ``Example.features.feature`` is a
 ``key -> feature`` dict whose values answer ``WhichOneof`` and expose the kind-checked lists.
@@ -8,7 +9,7 @@ An Example without a Features field has ``features = None`` (decoder.pyx:116,127
 from __future__ import annotations
 
 from tfr_reader import _status as S
-from tfr_reader import hip
+from tfr_reader import hip, host
 
 
 class Features:
@@ -26,7 +27,15 @@ class Example:
 
 
 def example_from_bytes(buffer) -> Example:
-    r = hip.decode_payloads([bytes(buffer)])
+    raw = bytes(buffer)
+    if len(raw) <= host.HOST_MAX_BYTES:
+        try:
+            return Example(Features(host.decode_dict(raw)))
+        except AttributeError:
+            if host.is_features_none(raw):
+                return Example(None)
+            raise
+    r = hip.decode_payloads([raw])
     if int(r.status[0]) == S.ERR_FEATURES_NONE:
         return Example(None)
     return Example(Features(r.record_dict(0)))

@@ -19,8 +19,9 @@ IndexFunc = Callable[["Feature"], dict[str, Any]]
 
 DecoderType = Literal["hip", "cython", "protobuf"]
 
-#: "hip" (default, libtfrg on the GPU); "cython" is accepted as an alias of "hip", whose results
-#: are bit-exact with the reference Cython decoder; "protobuf" uses google.protobuf (upb).
+#: "hip" (default: libtfrg, batches on the GPU, single records on the host); "cython" decodes every
+#: record on the host (libtfrg's host decode, bit-exact with the reference Cython decoder);
+#: "protobuf" uses google.protobuf (upb).
 TFRECORD_READER_DECODER_IMP: DecoderType = "hip"
 
 
@@ -66,8 +67,9 @@ _ACCESSORS: dict[str, type[BaseFeature]] = {
 
 
 class Feature:
-    """All features of one example, keyed by name, in the record's key order. (No ``__slots__``:
-    the device path's subclass is also a ``dict`` of accessors, tfr_reader/hip.py.)"""
+    """All features of one example, keyed by name, in the record's key order. The device path's
+    records are a subclass of this (tfr_reader/hip.py: a (batch, record, layout) tuple that pickles
+    as a plain ``Feature`` of its values)."""
 
     def __init__(self, feature):
         self.feature = feature
@@ -110,9 +112,19 @@ class Feature:
 
 # ------------------------------------------------------------------------------------ decoders
 def _hip_decode_fn(raw_record: bytes) -> Feature:
+    from tfr_reader import host  # noqa: PLC0415
+
+    if len(raw_record) <= host.HOST_MAX_BYTES:  # one record: far below the device's launch latency
+        return host.decode(raw_record)
     from tfr_reader import hip  # noqa: PLC0415
 
     return hip.decode_payloads([raw_record]).feature(0)
+
+
+def _cython_decode_fn(raw_record: bytes) -> Feature:
+    from tfr_reader import host  # noqa: PLC0415
+
+    return host.decode(raw_record)
 
 
 def _protobuf_decode_fn(raw_record: bytes) -> Feature:
@@ -126,8 +138,10 @@ def _protobuf_decode_fn(raw_record: bytes) -> Feature:
 def decode(raw_record: bytes) -> Feature:
     """Decode one serialized ``tf.train.Example`` payload."""
     imp = TFRECORD_READER_DECODER_IMP
-    if imp in ("hip", "cython"):
+    if imp == "hip":
         return _hip_decode_fn(raw_record)
+    if imp == "cython":
+        return _cython_decode_fn(raw_record)
     if imp == "protobuf":
         return _protobuf_decode_fn(raw_record)
     raise ValueError(f"Unknown decoder type: {imp}!")
@@ -137,6 +151,8 @@ def decode_batch(raw_records: list[bytes]) -> list[Feature]:
     """Decode many payloads in one device batch (raises the first failing record's exception)."""
     if TFRECORD_READER_DECODER_IMP == "protobuf":
         return [_protobuf_decode_fn(r) for r in raw_records]
+    if TFRECORD_READER_DECODER_IMP == "cython":
+        return [_cython_decode_fn(r) for r in raw_records]
     from tfr_reader import hip  # noqa: PLC0415
 
     return hip.decode_payloads(raw_records).features()

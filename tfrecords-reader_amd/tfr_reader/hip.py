@@ -10,7 +10,9 @@ pass on the first batch and costs nothing afterwards.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
+import gc
 import threading
 from collections.abc import Sequence
 
@@ -20,6 +22,19 @@ from tfr_reader import _native as N
 from tfr_reader import _status as S
 
 KIND_NAMES = {1: "bytes_list", 2: "float_list", 3: "int64_list"}
+
+
+@contextlib.contextmanager
+def _no_gc():
+    """Cyclic GC paused while a batch's Python objects are built: creating millions of lists and
+    tuples otherwise triggers generation scans over all of them (4-5x the construction time)."""
+    was = gc.isenabled()
+    gc.disable()
+    try:
+        yield
+    finally:
+        if was:
+            gc.enable()
 
 #: records larger than this (framed bytes) are decoded one wavefront per record (libtfrg default)
 DEFAULT_LANE_MAX = 2048
@@ -133,9 +148,6 @@ class HipDecoder:
         N.check(min(k, 0), "tfrg_learn_templates")
         return int(k)
 
-    def set_stage_count(self, on: bool) -> None:
-        """Count large staged records with k_stage_count (tfrg_ctx_set_stage_count; off by default)."""
-        N.check(self._lib.tfrg_ctx_set_stage_count(self._ctx, int(bool(on))), "tfrg_ctx_set_stage_count")
 
     def set_record_bound(self, nbytes: int) -> None:
         """Upper bound on (end - start) of the records of later ``decode_device`` calls (0 = unknown):
@@ -425,19 +437,23 @@ class BatchResult:
             py = self._py = [None] * len(self.slot_kind)
         c = py[s]
         if c is None:
-            base = int(self.slot_base[s])
-            rs = self.row_splits[s]
-            r0 = int(rs[0])
-            lo, hi = base + r0, base + int(rs[-1])
-            kind = self.slot_kind[s]
-            if kind == 3:
-                vals = self.i64[lo:hi].tolist()
-            elif kind == 2:
-                vals = self.f32[lo:hi].view(np.float32).tolist()
-            else:
-                vals = self._bytes_list(lo, hi)
-            c = py[s] = (vals, (rs - np.uint32(r0)).tolist() if r0 else rs.tolist())
+            with _no_gc():
+                c = py[s] = self._pycol_build(s)
         return c
+
+    def _pycol_build(self, s: int):
+        base = int(self.slot_base[s])
+        rs = self.row_splits[s]
+        r0 = int(rs[0])
+        lo, hi = base + r0, base + int(rs[-1])
+        kind = self.slot_kind[s]
+        if kind == 3:
+            vals = self.i64[lo:hi].tolist()
+        elif kind == 2:
+            vals = self.f32[lo:hi].view(np.float32).tolist()
+        else:
+            vals = self._bytes_list(lo, hi)
+        return vals, ((rs - np.uint32(r0)).tolist() if r0 else rs.tolist())
 
     def _bytes_list(self, lo: int, hi: int) -> list[bytes]:
         """bytes elements [lo, hi) as ``bytes``, sliced from one bytes copy of the region they span."""
@@ -495,7 +511,8 @@ class BatchResult:
             self._py = [None] * len(self.slot_kind)
         rec = _record_class()
         # one (batch, record, layout) tuple per record (built by tuple.__new__: no Python __init__)
-        return [rec((self, i, layouts[j])) for i, j in zip(range(start, stop), inv[start:stop].tolist())]
+        with _no_gc():
+            return [rec((self, i, layouts[j])) for i, j in zip(range(start, stop), inv[start:stop].tolist())]
 
     def column(self, key: str, kind: str | None = None) -> tuple[np.ndarray, np.ndarray]:
         """Ragged column of one key over the batch: (values, offsets) with record i's values at
@@ -736,6 +753,11 @@ def _record_class():
             @property
             def fields_names(self) -> list[str]:
                 return list(tuple.__getitem__(self, 2).keys)
+
+            def __reduce__(self):  # a plain Feature of the record's values (no batch reference)
+                r, i, lay = fields(self)
+                raw = {k: _ListRaw(KIND_NAMES[r.slot_kind[s]], r.slot_values(s, i)) for k, s in zip(lay.keys, lay.slots)}
+                return (Feature, (raw,))
 
             def __getitem__(self, key: str):
                 r, i, lay = fields(self)

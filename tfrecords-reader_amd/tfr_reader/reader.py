@@ -19,7 +19,7 @@ from pathlib import Path
 import numpy as np
 
 from tfr_reader import _frame as F
-from tfr_reader import _io, example, hip, indexer, logging
+from tfr_reader import _io, example, hip, host, indexer, logging
 
 LOGGER = logging.Logger(__name__)
 
@@ -67,7 +67,9 @@ def _check_path(path) -> None:
 
 def _decode_framed_bytes(data: bytes, start: int, end: int, dec=None) -> example.Feature:
     """Decode the framed record held in ``data`` (the bytes read for [start, end))."""
-    if example.feature.TFRECORD_READER_DECODER_IMP == "protobuf":
+    imp = example.feature.TFRECORD_READER_DECODER_IMP
+    if imp == "protobuf" or (dec is None and (imp == "cython" or len(data) <= host.HOST_MAX_BYTES)):
+        # one record: the host decode (reader.py:55 slices the framing off, no CRC check)
         return example.decode(data[12:-4])
     r = (dec or hip.default_decoder()).decode(data, [0], [end - start])
     return r.feature(0)
@@ -113,11 +115,21 @@ _LANE_DECODERS: dict = {}
 
 def set_devices(devices) -> None:
     """Default devices of ``load_ranges`` / ``load_records`` / ``__getitem__(Iterable)``: None (device
-    0), "all", an int or a list of device indices (tfr_reader.shard.resolve_devices)."""
+    0), "all", an int or a list of device indices (tfr_reader.shard.resolve_devices). Each (lane,
+    device) pair used keeps one decode context (its batch-sized device arenas) for the life of the
+    process, so the next call reuses it; ``release_lane_decoders()`` frees the extra ones."""
     global _DEFAULT_DEVICES
     from tfr_reader import shard
 
     _DEFAULT_DEVICES = None if devices is None else shard.resolve_devices(devices)
+
+
+def release_lane_decoders() -> None:
+    """Close the decode contexts of lanes > 0 (load_ranges with several lanes per device) and free
+    their device memory; the next call creates them again."""
+    for d in _LANE_DECODERS.values():
+        d.close()
+    _LANE_DECODERS.clear()
 
 
 def _lane_decoder(lane: int, device: int):
