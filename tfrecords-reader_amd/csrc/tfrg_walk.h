@@ -51,7 +51,7 @@ TFRG_WALK int skip_varint(S& s, int64_t& pos) {
 }
 
 struct Fld {
-  int64_t fn, wt, off, len;
+  int64_t fn = 0, wt = 0, off = 0, len = 0;
 };
 
 // One iteration of decode_message (decoder.pyx:69-104).

@@ -111,20 +111,29 @@ class Feature:
 
 
 # ------------------------------------------------------------------------------------ decoders
-def _hip_decode_fn(raw_record: bytes) -> Feature:
-    from tfr_reader import host  # noqa: PLC0415
+_HOST = None  # tfr_reader.host, imported on first use
 
+
+def _host():
+    global _HOST
+    if _HOST is None:
+        from tfr_reader import host  # noqa: PLC0415
+
+        _HOST = host
+    return _HOST
+
+
+def _hip_decode_fn(raw_record: bytes) -> Feature:
+    host = _HOST or _host()
     if len(raw_record) <= host.HOST_MAX_BYTES:  # one record: far below the device's launch latency
-        return host.decode(raw_record)
+        return Feature(host.decode_dict(raw_record))
     from tfr_reader import hip  # noqa: PLC0415
 
     return hip.decode_payloads([raw_record]).feature(0)
 
 
 def _cython_decode_fn(raw_record: bytes) -> Feature:
-    from tfr_reader import host  # noqa: PLC0415
-
-    return host.decode(raw_record)
+    return Feature((_HOST or _host()).decode_dict(raw_record))
 
 
 def _protobuf_decode_fn(raw_record: bytes) -> Feature:

@@ -18,6 +18,11 @@ from tfr_reader import _native as N
 from tfr_reader import _status as S
 from tfr_reader.hip import KIND_NAMES, _ListRaw
 
+try:  # the CPython binding (csrc/tfrg_py.cpp): host decode + the object graph built in C
+    from tfr_reader import _tfrg_py
+except ImportError:  # (built by make with the library; the ctypes path below needs libtfrg only)
+    _tfrg_py = None
+
 #: one-record calls of the "hip" decoder type with payloads up to this size are decoded here
 HOST_MAX_BYTES = 1 << 20
 
@@ -53,7 +58,25 @@ def _ctx() -> _Ctx:
 def decode_dict(raw, spec_varint: bool = False) -> dict:
     """``key -> raw feature`` of one payload (reference dict order); raises the record's exception
     (the reference's type and message, tfr_reader/_status.py)."""
-    raw = bytes(raw)
+    if type(raw) is not bytes:
+        raw = bytes(raw)
+    if _tfrg_py is not None:
+        res = _tfrg_py.decode(raw, N.FLAG_SPEC_VARINT if spec_varint else 0)
+        if type(res) is tuple:
+            _raise(raw, *res)
+        return res
+    return _decode_dict_ctypes(raw, spec_varint)
+
+
+def _raise(raw: bytes, st: int, aux: int):
+    key = None
+    if st == S.ERR_KEY_UTF8:
+        a = aux & 0xFFFFFFFFFFFFFFFF
+        key = raw[a >> 32 : (a >> 32) + (a & 0xFFFFFFFF)]
+    raise S.exception_for(st, aux, key)
+
+
+def _decode_dict_ctypes(raw: bytes, spec_varint: bool) -> dict:
     c = _ctx()
     rc = c.lib.tfrg_host_decode(c.h, raw, len(raw), N.FLAG_SPEC_VARINT if spec_varint else 0, c.rec_ref)
     if rc:

@@ -112,7 +112,18 @@ def create_index_for_tfrecord(tfrecord_path: str, index_fn: example.IndexFunc | 
     data["tfrecord_filename"].extend([filename] * n)
     data["tfrecord_start"].extend(ptrs[:, 0].tolist())
     data["tfrecord_end"].extend(ptrs[:, 1].tolist())
-    if index_fn is not None and n:
+    if index_fn is not None and n and example.feature.TFRECORD_READER_DECODER_IMP in ("cython", "protobuf"):
+        # record by record on the host, as indexer.py:96-100 (get_example + decode per record)
+        img = _io.file_image(tfrecord_path)
+        columnar = getattr(index_fn, "columnar", False)
+        for s, e in ptrs[:, :2].tolist():
+            if e > img.size:  # indexer.pyx:161-163
+                raise OSError("Failed to read record data")
+            f = example.decode(img[s + 12 : e - 4].tobytes())
+            row = index_fn.per_record(f) if columnar else index_fn(f)
+            for key, value in row.items():
+                data[key].append(value)
+    elif index_fn is not None and n:
         from tfr_reader.reader import _decode_bounded  # noqa: PLC0415 (reader imports this module)
 
         img = _io.file_image(tfrecord_path)

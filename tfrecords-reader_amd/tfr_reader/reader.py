@@ -162,10 +162,18 @@ def load_ranges(paths: Sequence[str], starts: Sequence[int], ends: Sequence[int]
     n = len(paths)
     out: list = [None] * n
     errors: list[BaseException | None] = [None] * n
-    if example.feature.TFRECORD_READER_DECODER_IMP == "protobuf":
+    if example.feature.TFRECORD_READER_DECODER_IMP in ("protobuf", "cython"):  # record by record on the host
+        imgs: dict = {}
         for i in range(n):
-            with TFRecordFileReader(paths[i]) as r:
-                out[i] = r.get_example(int(starts[i]), int(ends[i]))
+            img = imgs.get(paths[i])
+            if img is None:
+                _check_path(paths[i])
+                img = imgs[paths[i]] = _io.file_image(paths[i])
+            s, e = int(starts[i]), int(ends[i])
+            data = img[s:e].tobytes() if s < img.size else b""
+            if not data:
+                raise OSError(f"Failed to read data from {(s, e)}!")
+            out[i] = _decode_framed_bytes(data, s, e)
         return out
     starts = np.asarray(starts, np.uint64).reshape(-1)
     ends = np.asarray(ends, np.uint64).reshape(-1)
@@ -289,6 +297,7 @@ class TFRecordDatasetReader:
         self.index_df = F.with_row_index(index_df, "_row_id")
         self._sql = None
         self._cols = None  # (paths, file index per row, starts, ends), built on first access
+        self._files: dict = {}  # path -> ("fd", descriptor) | ("img", decompressed image), ds[i]
         self.logger.info(f"Loaded dataset index with N={F.height(self.index_df)} records ...")
 
     @property
@@ -344,9 +353,49 @@ class TFRecordDatasetReader:
             return load_ranges(*self._rows(idxs))
         if idx < 0 or idx >= self.size:
             raise IndexError(f"Index {idx=} out of bounds, dataset size={self.size}")
-        paths, starts, ends = self._rows([int(idx)])
-        with TFRecordFileReader(paths[0]) as reader:
-            return reader.get_example(int(starts[0]), int(ends[0]))
+        if self._cols is None:
+            self._rows([])
+        files, inv, st, en = self._cols
+        i = int(idx)
+        path, start, end = files[inv[i]], int(st[i]), int(en[i])
+        data = self._record_bytes(path, start, end)
+        if not data:
+            raise OSError(f"Failed to read data from {(start, end)}!")
+        return _decode_framed_bytes(data, start, end)
+
+    #: files kept open for ds[i] (the least recently opened are closed beyond this)
+    MAX_OPEN_FILES = 64
+
+    def _record_bytes(self, path: str, start: int, end: int) -> bytes:
+        """Bytes [start, end) of one file (reader.py:36-56 reads them with seek + read per call): a
+        plain file is read with one pread on a descriptor kept open by this dataset, a ZLIB / GZIP
+        file is sliced from its decompressed image (tfr_reader/_io.py)."""
+        h = self._files.get(path)
+        if h is None:
+            _check_path(path)
+            h = ("img", _io.file_image(path)) if _io.is_compressed(path) else ("fd", os.open(path, os.O_RDONLY))
+            if len(self._files) >= self.MAX_OPEN_FILES:
+                old = self._files.pop(next(iter(self._files)))
+                if old[0] == "fd":
+                    os.close(old[1])
+            self._files[path] = h
+        if h[0] == "fd":
+            return os.pread(h[1], max(end - start, 0), start) if end > start else b""
+        img = h[1]
+        return img[start:end].tobytes() if start < img.size else b""
+
+    def close(self) -> None:
+        """Close the file descriptors ds[i] keeps open."""
+        for kind, v in self._files.values():
+            if kind == "fd":
+                os.close(v)
+        self._files = {}
+
+    def __del__(self):  # noqa: D105
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
     def select(self, sql_query: str):
         selection = self.ctx.execute(sql_query)

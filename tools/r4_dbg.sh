@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# round-4 debugging on the GPU box: template hit rate, lean-kernel variants, then the hang trace
+set -u
+O=gpurun_out/r4d; mkdir -p $O
+timeout -k 5 90 python tools/dbg_r4.py c1 > $O/dbg_c1.log 2>&1 || { tail -20 $O/dbg_c1.log; exit 1; }
+tail -12 $O/dbg_c1.log
+for L in libtfrg.so libtfrg_nostore.so libtfrg_align4.so; do
+  TFRG_LIB=$PWD/tfrecords-reader_amd/tfr_reader/$L timeout -k 10 200 python bench.py --only c4of8 --no-cpu --steps 20 > $O/$L.json 2> $O/$L.err || { tail $O/$L.err; exit 1; }
+  python3 - "$O/$L.json" "$L" <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+print(sys.argv[2], d.get("value"), d["ms_per_step"], {k: round(v, 4) for k, v in d["kernels_ms"].items()})
+PY
+done
+AMD_LOG_LEVEL=3 HIP_LAUNCH_BLOCKING=1 timeout -k 5 60 python tools/dbg_r4.py spec > $O/dbg_spec.log 2>&1
+echo "spec rc=$?"
+grep -a "ShaderName\|^ok\|decoding" $O/dbg_spec.log | tail -12
