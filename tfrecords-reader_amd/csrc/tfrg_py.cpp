@@ -6,6 +6,7 @@
 // exposing the kind-checked float_list / int64_list / bytes_list whose .value is a fresh list per
 // access (cython/decoder.pyx:304-376). Built like the reference's own Cython module: a ctypes call
 // and Python-level object building cost several microseconds per record, this costs about one.
+// Also the C bases of the device path's Feature objects over a batch's columns (ColRec, ColAcc).
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
@@ -90,6 +91,238 @@ PyGetSetDef rf_getset[] = {{"float_list", (getter)rf_float, nullptr, nullptr, nu
                            {"kind", (getter)rf_kind, nullptr, nullptr, nullptr},
                            {nullptr}};
 PyTypeObject RawFeatureType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// ---- the device path's Feature objects over a batch's columns (tfr_reader/hip.py _record_class):
+// a record is (batch, record index, layout), f[key] an accessor over a slice [lo, hi) of the slot's
+// cached Python value list, .value that slice (a fresh list, feature.py:40-55). Python subclasses add
+// the reference classes as bases (Feature, Int64List / FloatList / BytesList).
+struct ColAcc {
+  PyObject_HEAD
+  PyObject* vals;  // list (null only for an instance made from Python: empty)
+  Py_ssize_t lo, hi;
+};
+
+void ca_dealloc(ColAcc* self) {
+  Py_XDECREF(self->vals);
+  Py_TYPE(self)->tp_free((PyObject*)self);
+}
+
+PyObject* ca_value(ColAcc* self, void*) {
+  if (!self->vals) return PyList_New(0);
+  return PyList_GetSlice(self->vals, self->lo, self->hi);
+}
+
+PyGetSetDef ca_getset[] = {{"value", (getter)ca_value, nullptr, nullptr, nullptr}, {nullptr}};
+PyTypeObject ColAccType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+struct ColRec {
+  PyObject_HEAD
+  PyObject* batch;  // BatchResult
+  PyObject* cols;   // batch._py: per slot None or (values list, row splits list)
+  PyObject* lay;    // _Layout
+  PyObject* acc;    // lay.acc: key -> (slot, accessor class)
+  PyObject* keys;   // lay.keys
+  Py_ssize_t i;
+};
+
+void cr_dealloc(ColRec* self) {
+  Py_XDECREF(self->batch);
+  Py_XDECREF(self->cols);
+  Py_XDECREF(self->lay);
+  Py_XDECREF(self->acc);
+  Py_XDECREF(self->keys);
+  Py_TYPE(self)->tp_free((PyObject*)self);
+}
+
+// f[key]: the accessor of key's slot over record i's slice (feature.py:100-110); a missing key raises
+// the reference's KeyError (feature.py:101-104)
+PyObject* cr_subscript(ColRec* self, PyObject* key) {
+  if (!self->acc) {
+    PyErr_SetString(PyExc_TypeError, "uninitialised Feature");
+    return nullptr;
+  }
+  PyObject* ent = PyDict_GetItemWithError(self->acc, key);
+  if (!ent) {
+    if (PyErr_Occurred()) return nullptr;
+    PyObject* msg = PyUnicode_FromFormat("Feature '%S' not found in the example, expected one of %R", key, self->keys);
+    if (msg) {
+      PyErr_SetObject(PyExc_KeyError, msg);
+      Py_DECREF(msg);
+    }
+    return nullptr;
+  }
+  const Py_ssize_t s = PyLong_AsSsize_t(PyTuple_GET_ITEM(ent, 0));
+  if (s < 0 || s >= PyList_GET_SIZE(self->cols)) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_IndexError, "slot out of range");
+    return nullptr;
+  }
+  PyObject* col = PyList_GET_ITEM(self->cols, s);
+  PyObject* owned = nullptr;
+  if (col == Py_None) {  // the slot's values as Python objects, converted once per batch
+    owned = col = PyObject_CallMethod(self->batch, "_pycol", "n", s);
+    if (!col) return nullptr;
+  }
+  PyObject* rs = PyTuple_GET_ITEM(col, 1);
+  PyObject* vals = PyTuple_GET_ITEM(col, 0);
+  Py_ssize_t lo = 0, hi = 0;
+  if (self->i + 1 < PyList_GET_SIZE(rs)) {
+    lo = PyLong_AsSsize_t(PyList_GET_ITEM(rs, self->i));
+    hi = PyLong_AsSsize_t(PyList_GET_ITEM(rs, self->i + 1));
+  }
+  PyTypeObject* cls = (PyTypeObject*)PyTuple_GET_ITEM(ent, 1);
+  ColAcc* a = (ColAcc*)cls->tp_alloc(cls, 0);
+  if (a) {
+    Py_INCREF(vals);
+    a->vals = vals;
+    a->lo = lo;
+    a->hi = hi;
+  }
+  Py_XDECREF(owned);
+  return (PyObject*)a;
+}
+
+Py_ssize_t cr_len(ColRec* self) { return self->keys ? PyList_GET_SIZE(self->keys) : 0; }
+
+PyObject* cr_fields_names(ColRec* self, void*) {
+  if (!self->keys) return PyList_New(0);
+  return PyList_GetSlice(self->keys, 0, PyList_GET_SIZE(self->keys));
+}
+PyObject* cr_batch(ColRec* self, void*) { return Py_NewRef(self->batch ? self->batch : Py_None); }
+PyObject* cr_lay(ColRec* self, void*) { return Py_NewRef(self->lay ? self->lay : Py_None); }
+PyObject* cr_index(ColRec* self, void*) { return PyLong_FromSsize_t(self->i); }
+
+PyMappingMethods cr_map = {(lenfunc)cr_len, (binaryfunc)cr_subscript, nullptr};
+PyGetSetDef cr_getset[] = {{"fields_names", (getter)cr_fields_names, nullptr, nullptr, nullptr},
+                           {"_batch", (getter)cr_batch, nullptr, nullptr, nullptr},
+                           {"_lay", (getter)cr_lay, nullptr, nullptr, nullptr},
+                           {"_i", (getter)cr_index, nullptr, nullptr, nullptr},
+                           {nullptr}};
+PyTypeObject ColRecType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// make_records(cls, batch, cols, start, inv, layouts) -> [cls record] for records start + j, j <
+// len(inv), record start + j having layout layouts[inv[j]] (inv: int64 buffer)
+PyObject* py_make_records(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 6 || !PyType_Check(args[0]) || !PyType_IsSubtype((PyTypeObject*)args[0], &ColRecType) ||
+      !PyList_Check(args[2]) || !PyList_Check(args[5])) {
+    PyErr_SetString(PyExc_TypeError, "make_records(cls, batch, cols: list, start: int, inv: int64 buffer, layouts: list)");
+    return nullptr;
+  }
+  PyTypeObject* cls = (PyTypeObject*)args[0];
+  const Py_ssize_t start = PyLong_AsSsize_t(args[3]);
+  if (start < 0) {
+    if (!PyErr_Occurred()) PyErr_SetString(PyExc_ValueError, "start < 0");
+    return nullptr;
+  }
+  Py_buffer vb;
+  if (PyObject_GetBuffer(args[4], &vb, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) < 0) return nullptr;
+  PyObject* out = nullptr;
+  const Py_ssize_t nl = PyList_GET_SIZE(args[5]);
+  PyObject** acc = nullptr;
+  PyObject** keys = nullptr;
+  if (vb.itemsize != 8 || !vb.format || (vb.format[0] != 'q' && vb.format[0] != 'l')) {
+    PyErr_SetString(PyExc_TypeError, "inv must be an int64 buffer");
+    goto done;
+  }
+  acc = (PyObject**)PyMem_Calloc(nl ? nl : 1, sizeof(PyObject*));
+  keys = (PyObject**)PyMem_Calloc(nl ? nl : 1, sizeof(PyObject*));
+  if (!acc || !keys) {
+    PyErr_NoMemory();
+    goto done;
+  }
+  for (Py_ssize_t l = 0; l < nl; ++l) {
+    acc[l] = PyObject_GetAttrString(PyList_GET_ITEM(args[5], l), "acc");
+    keys[l] = acc[l] ? PyObject_GetAttrString(PyList_GET_ITEM(args[5], l), "keys") : nullptr;
+    if (!keys[l]) goto done;
+    if (!PyDict_Check(acc[l]) || !PyList_Check(keys[l])) {
+      PyErr_SetString(PyExc_TypeError, "layout.acc must be a dict and layout.keys a list");
+      goto done;
+    }
+  }
+  {
+    const int64_t* inv = (const int64_t*)vb.buf;
+    const Py_ssize_t n = vb.len / 8;
+    out = PyList_New(n);
+    if (!out) goto done;
+    for (Py_ssize_t j = 0; j < n; ++j) {
+      const int64_t l = inv[j];
+      if (l < 0 || l >= nl) {
+        PyErr_SetString(PyExc_IndexError, "layout index out of range");
+        Py_CLEAR(out);
+        goto done;
+      }
+      ColRec* r = (ColRec*)cls->tp_alloc(cls, 0);
+      if (!r) {
+        Py_CLEAR(out);
+        goto done;
+      }
+      r->batch = Py_NewRef(args[1]);
+      r->cols = Py_NewRef(args[2]);
+      r->lay = Py_NewRef(PyList_GET_ITEM(args[5], l));
+      r->acc = Py_NewRef(acc[l]);
+      r->keys = Py_NewRef(keys[l]);
+      r->i = start + j;
+      PyList_SET_ITEM(out, j, (PyObject*)r);
+    }
+  }
+done:
+  if (acc)
+    for (Py_ssize_t l = 0; l < nl; ++l) {
+      Py_XDECREF(acc[l]);
+      Py_XDECREF(keys[l]);
+    }
+  PyMem_Free(acc);
+  PyMem_Free(keys);
+  PyBuffer_Release(&vb);
+  return out;
+}
+
+// split_bytes(buf, off, len) -> [bytes(buf[off[j]:off[j] + len[j]])] (off, len: int64 buffers): a
+// bytes_list column's elements as Python bytes, copied straight from the batch's buffer
+PyObject* py_split_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "split_bytes(buf, off: int64 buffer, len: int64 buffer)");
+    return nullptr;
+  }
+  Py_buffer b, ob, lb;
+  if (PyObject_GetBuffer(args[0], &b, PyBUF_C_CONTIGUOUS) < 0) return nullptr;
+  if (PyObject_GetBuffer(args[1], &ob, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) < 0) {
+    PyBuffer_Release(&b);
+    return nullptr;
+  }
+  if (PyObject_GetBuffer(args[2], &lb, PyBUF_C_CONTIGUOUS | PyBUF_FORMAT) < 0) {
+    PyBuffer_Release(&ob);
+    PyBuffer_Release(&b);
+    return nullptr;
+  }
+  PyObject* out = nullptr;
+  auto i64 = [](const Py_buffer& v) { return v.itemsize == 8 && v.format && (v.format[0] == 'q' || v.format[0] == 'l'); };
+  if (!i64(ob) || !i64(lb) || ob.len != lb.len) {
+    PyErr_SetString(PyExc_TypeError, "off and len must be int64 buffers of one length");
+  } else {
+    const int64_t* o = (const int64_t*)ob.buf;
+    const int64_t* l = (const int64_t*)lb.buf;
+    const Py_ssize_t n = ob.len / 8;
+    const char* p = (const char*)b.buf;
+    out = PyList_New(n);
+    for (Py_ssize_t j = 0; out && j < n; ++j) {
+      if (o[j] < 0 || l[j] < 0 || o[j] > b.len || l[j] > b.len - o[j]) {
+        PyErr_SetString(PyExc_IndexError, "bytes element outside the buffer");
+        Py_CLEAR(out);
+        break;
+      }
+      PyObject* x = PyBytes_FromStringAndSize(p + o[j], l[j]);
+      if (!x) {
+        Py_CLEAR(out);
+        break;
+      }
+      PyList_SET_ITEM(out, j, x);
+    }
+  }
+  PyBuffer_Release(&lb);
+  PyBuffer_Release(&ob);
+  PyBuffer_Release(&b);
+  return out;
+}
 
 // one host context per thread (its result arrays are reused call after call)
 struct TlsCtx {
@@ -188,6 +421,8 @@ PyObject* py_raw_feature(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
 
 PyMethodDef methods[] = {{"decode", (PyCFunction)(void (*)(void))py_decode, METH_FASTCALL, nullptr},
                          {"raw_feature", (PyCFunction)(void (*)(void))py_raw_feature, METH_FASTCALL, nullptr},
+                         {"make_records", (PyCFunction)(void (*)(void))py_make_records, METH_FASTCALL, nullptr},
+                         {"split_bytes", (PyCFunction)(void (*)(void))py_split_bytes, METH_FASTCALL, nullptr},
                          {nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_tfrg_py", nullptr, -1, methods};
@@ -213,15 +448,31 @@ PyMODINIT_FUNC PyInit__tfrg_py(void) {
   RawFeatureType.tp_flags = Py_TPFLAGS_DEFAULT;
   RawFeatureType.tp_methods = rf_methods;
   RawFeatureType.tp_getset = rf_getset;
-  if (PyType_Ready(&ValueListType) < 0 || PyType_Ready(&BytesValueListType) < 0 || PyType_Ready(&RawFeatureType) < 0)
+  ColAccType.tp_name = "tfr_reader._tfrg_py.ColAcc";
+  ColAccType.tp_basicsize = sizeof(ColAcc);
+  ColAccType.tp_dealloc = (destructor)ca_dealloc;
+  ColAccType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE;
+  ColAccType.tp_getset = ca_getset;
+  ColRecType.tp_name = "tfr_reader._tfrg_py.ColRec";
+  ColRecType.tp_basicsize = sizeof(ColRec);
+  ColRecType.tp_dealloc = (destructor)cr_dealloc;
+  ColRecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE;
+  ColRecType.tp_getset = cr_getset;
+  ColRecType.tp_as_mapping = &cr_map;
+  if (PyType_Ready(&ValueListType) < 0 || PyType_Ready(&BytesValueListType) < 0 || PyType_Ready(&RawFeatureType) < 0 ||
+      PyType_Ready(&ColAccType) < 0 || PyType_Ready(&ColRecType) < 0)
     return nullptr;
   PyObject* m = PyModule_Create(&module);
   if (!m) return nullptr;
-  Py_INCREF(&RawFeatureType);
-  if (PyModule_AddObject(m, "RawFeature", (PyObject*)&RawFeatureType) < 0) {
-    Py_DECREF(&RawFeatureType);
-    Py_DECREF(m);
-    return nullptr;
+  PyTypeObject* types[] = {&RawFeatureType, &ColAccType, &ColRecType};
+  const char* names[] = {"RawFeature", "ColAcc", "ColRec"};
+  for (int t = 0; t < 3; ++t) {
+    Py_INCREF(types[t]);
+    if (PyModule_AddObject(m, names[t], (PyObject*)types[t]) < 0) {
+      Py_DECREF(types[t]);
+      Py_DECREF(m);
+      return nullptr;
+    }
   }
   return m;
 }

@@ -66,10 +66,10 @@ _ACCESSORS: dict[str, type[BaseFeature]] = {
 }
 
 
-class Feature:
+class Feature(metaclass=abc.ABCMeta):
     """All features of one example, keyed by name, in the record's key order. The device path's
-    records are a subclass of this (tfr_reader/hip.py: a (batch, record, layout) tuple that pickles
-    as a plain ``Feature`` of its values)."""
+    records are registered subclasses of this (tfr_reader/hip.py: (batch, record, layout) objects
+    over the batch's columns that pickle as a plain ``Feature`` of their values)."""
 
     def __init__(self, feature):
         self.feature = feature

@@ -21,6 +21,11 @@ import numpy as np
 from tfr_reader import _native as N
 from tfr_reader import _status as S
 
+try:  # C bases of the Feature objects over a batch's columns (csrc/tfrg_py.cpp, built with libtfrg)
+    from tfr_reader import _tfrg_py as _PY
+except ImportError:
+    _PY = None
+
 KIND_NAMES = {1: "bytes_list", 2: "float_list", 3: "int64_list"}
 
 
@@ -369,6 +374,13 @@ class BatchResult:
 
     def _bytes_elems(self, lo: int, hi: int) -> list[bytes]:
         """bytes elements [lo, hi) of the bytes value array, as ``bytes``."""
+        if hi <= lo:
+            return []
+        if _PY is not None:  # (copied in C straight from the buffer)
+            if self.bytes_data is not None:
+                o = self.bytes_offsets[lo : hi + 1].astype(np.int64)
+                return _PY.split_bytes(self.bytes_data, o[:-1], np.diff(o))
+            return _PY.split_bytes(self.buf, self.bytes_off[lo:hi].astype(np.int64), self.bytes_len[lo:hi].astype(np.int64))
         if self.bytes_data is not None:
             o = self.bytes_offsets[lo : hi + 1].tolist()
             d = self.bytes_data
@@ -426,6 +438,8 @@ class BatchResult:
         inv, layouts = self._lay
         if self._py is None:
             self._py = [None] * len(self.slot_kind)
+        if _PY is not None:
+            return _PY.make_records(_record_class(), self, self._py, i, inv[i : i + 1], layouts)[0]
         return _record_class()((self, i, layouts[int(inv[i])]))
 
     def _pycol(self, s: int):
@@ -459,6 +473,8 @@ class BatchResult:
         """bytes elements [lo, hi) as ``bytes``, sliced from one bytes copy of the region they span."""
         if hi <= lo:
             return []
+        if _PY is not None:
+            return self._bytes_elems(lo, hi)
         if self.bytes_data is not None:
             o = self.bytes_offsets[lo : hi + 1]
             a = int(o[0])
@@ -510,8 +526,10 @@ class BatchResult:
         if self._py is None:
             self._py = [None] * len(self.slot_kind)
         rec = _record_class()
-        # one (batch, record, layout) tuple per record (built by tuple.__new__: no Python __init__)
         with _no_gc():
+            if _PY is not None:  # records made in C
+                return _PY.make_records(rec, self, self._py, start, inv[start:stop], layouts)
+            # one (batch, record, layout) tuple per record (built by tuple.__new__: no Python __init__)
             return [rec((self, i, layouts[j])) for i, j in zip(range(start, stop), inv[start:stop].tolist())]
 
     def column(self, key: str, kind: str | None = None) -> tuple[np.ndarray, np.ndarray]:
@@ -698,6 +716,17 @@ def _accessor_classes() -> dict:
         from tfr_reader.example import feature as F  # noqa: PLC0415
 
         def make(base, kind):
+            if _PY is not None:
+                # C base (csrc/tfrg_py.cpp ColAcc): made and read without bytecode, no __dict__ and
+                # no GC tracking per object; an instance of ``base`` by ABC registration
+                ns = {"__slots__": (), "feature": property(lambda self: _ListRaw(kind, self.value))}
+                if base is F.BytesList:
+                    ns["bytes_io"] = F.BytesList.bytes_io
+                CAcc = type(base.__name__, (_PY.ColAcc,), ns)
+                CAcc.__qualname__ = base.__name__
+                base.register(CAcc)
+                return CAcc
+
             # a (values, lo, hi) tuple: created by tuple.__new__ alone (no Python __init__ per access)
             class Acc(tuple, base):
                 __slots__ = ()
@@ -728,6 +757,36 @@ def _record_class():
     global _RECORD_CLASS
     if _RECORD_CLASS is None:
         from tfr_reader.example.feature import Feature  # noqa: PLC0415
+
+        if _PY is not None:
+            # C base (csrc/tfrg_py.cpp ColRec): f[key], len(f), f.fields_names in C, no __dict__ and
+            # no GC tracking per record; Feature's own methods, and an instance of Feature by ABC
+            # registration
+            class CFeature(_PY.ColRec):
+                __slots__ = ()
+                __eq__ = Feature.__eq__
+                __ne__ = lambda self, other: not self == other  # noqa: E731
+                __hash__ = None
+                __repr__ = Feature.__repr__
+                as_dict = Feature.as_dict
+                fields = Feature.fields
+
+                @property
+                def feature(self):  # the reference's key -> raw feature mapping
+                    return _RecordView(self._batch, self._i, self._lay)
+
+                def __iter__(self):  # (the reference's Feature has no iteration of its own)
+                    raise TypeError("'Feature' object is not iterable")
+
+                def __reduce__(self):  # a plain Feature of the record's values (no batch reference)
+                    r, i, lay = self._batch, self._i, self._lay
+                    raw = {k: _ListRaw(KIND_NAMES[r.slot_kind[s]], r.slot_values(s, i)) for k, s in zip(lay.keys, lay.slots)}
+                    return (Feature, (raw,))
+
+            CFeature.__name__ = CFeature.__qualname__ = "Feature"
+            Feature.register(CFeature)
+            _RECORD_CLASS = CFeature
+            return _RECORD_CLASS
 
         fields = tuple.__iter__  # (C-level unpacking: __getitem__ is the feature lookup here)
 
