@@ -1356,6 +1356,10 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + cnt_words);              // [n_slots][kLaneCountBlock]
   const uint32_t ord_bytes = GORD ? 0u : ((S * kLaneCountBlock * 2u + 15u) & ~15u);
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // residual mode: a workgroup with no listed group exits before loading its tables (block-uniform)
+  const bool resid = o.rlist != nullptr;
+  const uint32_t nres = resid ? rfl32(o.info[kInfoResid]) : 0u;
+  if (resid && blockIdx.x * kWaves >= nres) return;
   uint8_t* stage_all = reinterpret_cast<uint8_t*>(ord) + ord_bytes;
   uint8_t* stage = stage_all + wib * kStageStride;
   uint32_t* kht = reinterpret_cast<uint32_t*>(stage_all + kWaves * kStageStride);
@@ -1383,8 +1387,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
 
   // 64-record groups: group g of the batch, or (residual mode) the g-th listed group with its mask
-  const bool resid = o.rlist != nullptr;
-  const uint32_t nres = resid ? rfl32(o.info[kInfoResid]) : 0u;
   const uint32_t nw = gridDim.x * kWaves;
   auto group = [&](uint32_t g, uint64_t& gb, uint64_t& gm) -> bool {
     if (resid) {

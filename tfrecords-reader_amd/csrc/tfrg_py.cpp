@@ -276,6 +276,85 @@ done:
   return out;
 }
 
+// ---- a host-decoded record as the reference's Feature (feature.py:69-110) over its key -> raw feature
+// dict: f[key] makes the accessor (the ColAcc subclass of the key's kind over the raw feature's value
+// list) in C. Python subclass: tfr_reader/host.py.
+struct HostRec {
+  PyObject_HEAD
+  PyObject* dict;
+};
+
+PyTypeObject* g_acc[4] = {nullptr, nullptr, nullptr, nullptr};  // accessor class per kind (set_accessors)
+PyTypeObject* g_host_cls = nullptr;                               // HostRec subclass (set_accessors)
+
+void hr_dealloc(HostRec* self) {
+  Py_XDECREF(self->dict);
+  Py_TYPE(self)->tp_free((PyObject*)self);
+}
+
+PyObject* hr_subscript(HostRec* self, PyObject* key) {
+  if (!self->dict) {
+    PyErr_SetString(PyExc_TypeError, "uninitialised Feature");
+    return nullptr;
+  }
+  PyObject* raw = PyDict_GetItemWithError(self->dict, key);
+  if (!raw) {
+    if (PyErr_Occurred()) return nullptr;
+    PyObject* keys = PyDict_Keys(self->dict);
+    if (!keys) return nullptr;
+    PyObject* msg = PyUnicode_FromFormat("Feature '%S' not found in the example, expected one of %R", key, keys);
+    Py_DECREF(keys);
+    if (msg) {
+      PyErr_SetObject(PyExc_KeyError, msg);
+      Py_DECREF(msg);
+    }
+    return nullptr;
+  }
+  if (Py_TYPE(raw) != &RawFeatureType) {
+    PyErr_SetString(PyExc_TypeError, "not a raw feature of the host decode");
+    return nullptr;
+  }
+  RawFeature* rf = (RawFeature*)raw;
+  PyTypeObject* cls = g_acc[rf->kind];
+  if (!cls) {
+    PyErr_SetString(PyExc_RuntimeError, "set_accessors() was not called");
+    return nullptr;
+  }
+  ColAcc* a = (ColAcc*)cls->tp_alloc(cls, 0);
+  if (!a) return nullptr;
+  Py_INCREF(rf->values);
+  a->vals = rf->values;
+  a->lo = 0;
+  a->hi = PyList_GET_SIZE(rf->values);
+  return (PyObject*)a;
+}
+
+Py_ssize_t hr_len(HostRec* self) { return self->dict ? PyDict_GET_SIZE(self->dict) : 0; }
+PyObject* hr_feature(HostRec* self, void*) { return Py_NewRef(self->dict ? self->dict : Py_None); }
+PyObject* hr_fields_names(HostRec* self, void*) { return self->dict ? PyDict_Keys(self->dict) : PyList_New(0); }
+
+PyMappingMethods hr_map = {(lenfunc)hr_len, (binaryfunc)hr_subscript, nullptr};
+PyGetSetDef hr_getset[] = {{"feature", (getter)hr_feature, nullptr, nullptr, nullptr},
+                           {"fields_names", (getter)hr_fields_names, nullptr, nullptr, nullptr},
+                           {nullptr}};
+PyTypeObject HostRecType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+// set_accessors(host_cls, bytes_acc, float_acc, int64_acc): the Python classes the C paths create
+PyObject* py_set_accessors(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 4 || !PyType_Check(args[0]) || !PyType_IsSubtype((PyTypeObject*)args[0], &HostRecType)) {
+    PyErr_SetString(PyExc_TypeError, "set_accessors(host_cls, bytes_acc, float_acc, int64_acc)");
+    return nullptr;
+  }
+  for (int k = 1; k <= 3; ++k)
+    if (!PyType_Check(args[k]) || !PyType_IsSubtype((PyTypeObject*)args[k], &ColAccType)) {
+      PyErr_SetString(PyExc_TypeError, "accessor classes must subclass ColAcc");
+      return nullptr;
+    }
+  Py_XSETREF(g_host_cls, (PyTypeObject*)Py_NewRef(args[0]));
+  for (int k = 1; k <= 3; ++k) Py_XSETREF(g_acc[k], (PyTypeObject*)Py_NewRef(args[k]));
+  Py_RETURN_NONE;
+}
+
 // split_bytes(buf, off, len) -> [bytes(buf[off[j]:off[j] + len[j]])] (off, len: int64 buffers): a
 // bytes_list column's elements as Python bytes, copied straight from the batch's buffer
 PyObject* py_split_bytes(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
@@ -358,14 +437,10 @@ PyObject* values_of(const tfrg_host_record& r, uint32_t e, const char* raw) {
 }
 
 // decode(raw: bytes, flags: int) -> dict (key -> raw feature) | (status, aux) for a failing record
-PyObject* py_decode(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-  if (nargs != 2 || !PyBytes_Check(args[0])) {
-    PyErr_SetString(PyExc_TypeError, "decode(raw: bytes, flags: int)");
-    return nullptr;
-  }
-  const char* raw = PyBytes_AS_STRING(args[0]);
-  const Py_ssize_t len = PyBytes_GET_SIZE(args[0]);
-  const unsigned long flags = PyLong_AsUnsignedLong(args[1]);
+PyObject* decode_impl(PyObject* rawobj, PyObject* flagobj) {
+  const char* raw = PyBytes_AS_STRING(rawobj);
+  const Py_ssize_t len = PyBytes_GET_SIZE(rawobj);
+  const unsigned long flags = PyLong_AsUnsignedLong(flagobj);
   if (PyErr_Occurred()) return nullptr;
   if (!tls.c && tfrg_host_ctx_create(&tls.c) != 0) return PyErr_NoMemory();
   tfrg_host_record r;
@@ -400,6 +475,35 @@ PyObject* py_decode(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return d;
 }
 
+PyObject* py_decode(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyBytes_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "decode(raw: bytes, flags: int)");
+    return nullptr;
+  }
+  return decode_impl(args[0], args[1]);
+}
+
+// decode_feature(raw: bytes, flags: int) -> Feature (the set_accessors host class) | (status, aux)
+PyObject* py_decode_feature(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyBytes_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "decode_feature(raw: bytes, flags: int)");
+    return nullptr;
+  }
+  if (!g_host_cls) {
+    PyErr_SetString(PyExc_RuntimeError, "set_accessors() was not called");
+    return nullptr;
+  }
+  PyObject* d = decode_impl(args[0], args[1]);
+  if (!d || !PyDict_Check(d)) return d;
+  HostRec* f = (HostRec*)g_host_cls->tp_alloc(g_host_cls, 0);
+  if (!f) {
+    Py_DECREF(d);
+    return nullptr;
+  }
+  f->dict = d;
+  return (PyObject*)f;
+}
+
 // raw_feature(kind: int, values: list) -> raw feature (the device path's records pickled, and tests)
 PyObject* py_raw_feature(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   if (nargs != 2 || !PyList_Check(args[1])) {
@@ -423,6 +527,8 @@ PyMethodDef methods[] = {{"decode", (PyCFunction)(void (*)(void))py_decode, METH
                          {"raw_feature", (PyCFunction)(void (*)(void))py_raw_feature, METH_FASTCALL, nullptr},
                          {"make_records", (PyCFunction)(void (*)(void))py_make_records, METH_FASTCALL, nullptr},
                          {"split_bytes", (PyCFunction)(void (*)(void))py_split_bytes, METH_FASTCALL, nullptr},
+                         {"set_accessors", (PyCFunction)(void (*)(void))py_set_accessors, METH_FASTCALL, nullptr},
+                         {"decode_feature", (PyCFunction)(void (*)(void))py_decode_feature, METH_FASTCALL, nullptr},
                          {nullptr}};
 
 PyModuleDef module = {PyModuleDef_HEAD_INIT, "_tfrg_py", nullptr, -1, methods};
@@ -459,14 +565,20 @@ PyMODINIT_FUNC PyInit__tfrg_py(void) {
   ColRecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE;
   ColRecType.tp_getset = cr_getset;
   ColRecType.tp_as_mapping = &cr_map;
+  HostRecType.tp_name = "tfr_reader._tfrg_py.HostRec";
+  HostRecType.tp_basicsize = sizeof(HostRec);
+  HostRecType.tp_dealloc = (destructor)hr_dealloc;
+  HostRecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE;
+  HostRecType.tp_getset = hr_getset;
+  HostRecType.tp_as_mapping = &hr_map;
   if (PyType_Ready(&ValueListType) < 0 || PyType_Ready(&BytesValueListType) < 0 || PyType_Ready(&RawFeatureType) < 0 ||
-      PyType_Ready(&ColAccType) < 0 || PyType_Ready(&ColRecType) < 0)
+      PyType_Ready(&ColAccType) < 0 || PyType_Ready(&ColRecType) < 0 || PyType_Ready(&HostRecType) < 0)
     return nullptr;
   PyObject* m = PyModule_Create(&module);
   if (!m) return nullptr;
-  PyTypeObject* types[] = {&RawFeatureType, &ColAccType, &ColRecType};
-  const char* names[] = {"RawFeature", "ColAcc", "ColRec"};
-  for (int t = 0; t < 3; ++t) {
+  PyTypeObject* types[] = {&RawFeatureType, &ColAccType, &ColRecType, &HostRecType};
+  const char* names[] = {"RawFeature", "ColAcc", "ColRec", "HostRec"};
+  for (int t = 0; t < 4; ++t) {
     Py_INCREF(types[t]);
     if (PyModule_AddObject(m, names[t], (PyObject*)types[t]) < 0) {
       Py_DECREF(types[t]);

@@ -126,14 +126,14 @@ def _host():
 def _hip_decode_fn(raw_record: bytes) -> Feature:
     host = _HOST or _host()
     if len(raw_record) <= host.HOST_MAX_BYTES:  # one record: far below the device's launch latency
-        return Feature(host.decode_dict(raw_record))
+        return host.decode(raw_record)
     from tfr_reader import hip  # noqa: PLC0415
 
     return hip.decode_payloads([raw_record]).feature(0)
 
 
 def _cython_decode_fn(raw_record: bytes) -> Feature:
-    return Feature((_HOST or _host()).decode_dict(raw_record))
+    return (_HOST or _host()).decode(raw_record)
 
 
 def _protobuf_decode_fn(raw_record: bytes) -> Feature:

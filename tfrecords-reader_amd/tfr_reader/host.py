@@ -132,8 +132,52 @@ def decode_raw(raw, spec_varint: bool = False) -> tuple[int, int, list]:
     return 0, 0, ents
 
 
+_HOST_CLS = None
+
+
+def _host_class():
+    """The host path's ``Feature``: the C type HostRec (csrc/tfrg_py.cpp: ``f[key]`` makes the
+    ``Int64List`` / ``FloatList`` / ``BytesList`` accessor in C) with Feature's own methods, an
+    instance of Feature by ABC registration; pickles as a plain Feature of its raw features."""
+    global _HOST_CLS
+    if _HOST_CLS is None:
+        from tfr_reader.example.feature import Feature  # noqa: PLC0415
+        from tfr_reader.hip import _accessor_classes  # noqa: PLC0415
+
+        class HostFeature(_tfrg_py.HostRec):
+            __slots__ = ()
+            __eq__ = Feature.__eq__
+            __ne__ = lambda self, other: not self == other  # noqa: E731
+            __hash__ = None
+            __repr__ = Feature.__repr__
+            as_dict = Feature.as_dict
+            fields = Feature.fields
+
+            def __iter__(self):  # (the reference's Feature has no iteration of its own)
+                raise TypeError("'Feature' object is not iterable")
+
+            def __reduce__(self):
+                return (Feature, (self.feature,))
+
+        HostFeature.__name__ = HostFeature.__qualname__ = "Feature"
+        Feature.register(HostFeature)
+        acc = _accessor_classes()
+        _tfrg_py.set_accessors(HostFeature, acc[1], acc[2], acc[3])
+        _HOST_CLS = HostFeature
+    return _HOST_CLS
+
+
 def decode(raw, spec_varint: bool = False):
     """One payload as a ``Feature`` (the reference's decode(), example/feature.py:146-151)."""
+    if _tfrg_py is not None:
+        if _HOST_CLS is None:
+            _host_class()
+        if type(raw) is not bytes:
+            raw = bytes(raw)
+        res = _tfrg_py.decode_feature(raw, N.FLAG_SPEC_VARINT if spec_varint else 0)
+        if type(res) is tuple:
+            _raise(raw, *res)
+        return res
     from tfr_reader.example.feature import Feature  # noqa: PLC0415
 
     return Feature(decode_dict(raw, spec_varint))

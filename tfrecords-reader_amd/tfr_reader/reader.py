@@ -343,6 +343,18 @@ class TFRecordDatasetReader:
         return [files[k] for k in inv[ii].tolist()], st[ii], en[ii]
 
     def __getitem__(self, idx):
+        if type(idx) is int and self._cols is not None:  # (one record: no ABC check, no frame access)
+            files, inv, st, en = self._cols
+            if idx < 0 or idx >= st.shape[0]:
+                raise IndexError(f"Index {idx=} out of bounds, dataset size={self.size}")
+            start, end = int(st[idx]), int(en[idx])
+            path = files[inv[idx]]
+            h = self._files.get(path)
+            if h is not None and h[0] == "fd" and end - start > 16 and end - start - 16 <= host.HOST_MAX_BYTES \
+                    and example.feature.TFRECORD_READER_DECODER_IMP != "protobuf":
+                data = os.pread(h[1], end - start, start)
+                if len(data) == end - start:  # (else the general path below reports it)
+                    return host.decode(data[12:-4])
         if isinstance(idx, Iterable):
             idxs = [int(i) for i in idx]
             for i in idxs:

@@ -22,12 +22,18 @@ def c1_payloads(n: int, offset: int = 0) -> list[bytes]:
     ]
 
 
-def c2_payloads(n: int = 8189, seed: int = 2, scale: float = 1.0) -> list[bytes]:
+def c2_truth(n: int = 8189, seed: int = 2, scale: float = 1.0) -> tuple[np.ndarray, bytes, np.ndarray]:
+    """The random draws of ``c2_payloads``: (image sizes, the images concatenated, labels)."""
     rng = np.random.default_rng(seed)
     sizes = np.clip(rng.lognormal(np.log(40960), 0.5, n), 4096, 524288).astype(np.int64)
     sizes = np.maximum((sizes * scale).astype(np.int64), 16)
     blob = rng.integers(0, 256, int(sizes.sum()), dtype=np.uint8).tobytes()
     labels = rng.integers(0, 102, n)
+    return sizes, blob, labels
+
+
+def c2_payloads(n: int = 8189, seed: int = 2, scale: float = 1.0) -> list[bytes]:
+    sizes, blob, labels = c2_truth(n, seed, scale)
     out, p = [], 0
     for i in range(n):
         img = blob[p : p + sizes[i]]

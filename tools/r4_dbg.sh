@@ -1,5 +1,6 @@
 #!/usr/bin/env bash
-# round-4 debugging on the GPU box: template hit rate, lean-kernel variants, then the hang trace
+# round-4 debugging on the GPU box: template hit rate, lean-kernel variants, the hang trace, then
+# (only if that ran clean) the GPU suite
 set -u
 O=gpurun_out/r4d; mkdir -p $O
 timeout -k 5 90 python tools/dbg_r4.py c1 > $O/dbg_c1.log 2>&1 || { tail -20 $O/dbg_c1.log; exit 1; }
@@ -13,5 +14,11 @@ print(sys.argv[2], d.get("value"), d["ms_per_step"], {k: round(v, 4) for k, v in
 PY
 done
 AMD_LOG_LEVEL=3 HIP_LAUNCH_BLOCKING=1 timeout -k 5 60 python tools/dbg_r4.py spec > $O/dbg_spec.log 2>&1
-echo "spec rc=$?"
+rc=$?
+echo "spec rc=$rc"
 grep -a "ShaderName\|^ok\|decoding" $O/dbg_spec.log | tail -12
+[ $rc -eq 0 ] || exit 1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+rc=$?
+tail -40 $O/tests.log
+exit $rc
