@@ -66,13 +66,14 @@ struct LeanTgt {
   uint32_t* v2;    // speculative placement of bytes: the length column at n * (rank - 1)
   uint32_t lim;    // speculative placement: records r < lim are stored (capacity)
   uint32_t kind;   // speculative placement kind (0: the slot is not placed speculatively)
-  uint32_t tsum;   // slot * tile_stride
-  uint32_t pad;
+  uint32_t pad[2];
 };
 struct LeanArgs {
   uint32_t n_tpl;
   uint32_t lane_max;
-  uint32_t* tsum;
+  uint32_t* tsum;  // tile sums, slot k's at k * tile_stride
+  uint32_t n_slots;
+  uint32_t tile_stride;
   LeanTgt tg[kLeanMaxSlots];
 };
 
@@ -131,6 +132,7 @@ enum InfoIdx : uint32_t {
   kInfoCrcCtr = 14,      // [14..15] u64: streaming-CRC list entries << kCrcIdxShift | flat 1 KiB rounds
   kInfoDefer = 16,       // k_lane_count: 64-record rows of deferred packed-int64 bodies reserved (k_body_count)
   kInfoResid = 17,       // k_tpl_lane: 64-record groups listed for k_lane_count (records no template took)
+  kInfoGatherDone = 18,  // k_list_gather workgroups finished (the last one clears irr for the next decode)
   kInfoCount = 20
 };
 
@@ -186,7 +188,7 @@ struct DevOut {
   uint64_t* crc_base;    // [n] its first flat round (ascending with the list index)
   uint64_t* crc_part;    // [n] rounds done << 32 | XOR of the slices, of a record split over waves
   uint32_t* irr;         // [n_slots] records not placed speculatively per slot (DevSchema::spec; after
-                         // the scan words in their buffer, zero between decodes: k_tail_gather clears)
+                         // the scan words in their buffer, zero between decodes: k_list_gather clears)
   uint4* dq;             // [dq_blocks][64][kDeferK] deferred bodies (nullptr: no deferral this decode)
   uint8_t* dq_cnt;       // [dq_blocks][64] entries used per row (0 for records not accepted)
   uint32_t dq_blocks;
@@ -242,7 +244,7 @@ struct LaunchCfg {
 
 // Kernel stages, in launch order (profiling events bracket each one).
 enum Stage : int { kStageTplLane = 0, kStageLaneCount, kStageBodyCount, kStageTailCount, kStageSpine,
-                   kStageDownGather, kStageTailGather, kStageMaterialize, kNumStages };
+                   kStageDownGather, kStageListGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

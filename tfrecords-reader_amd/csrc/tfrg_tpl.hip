@@ -94,38 +94,70 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)B.nbytes, 0x00020000);
   const uint32_t ngroups = (B.n + 63u) >> 6;
+  // A wave takes whole 256-record tiles (4 groups of 64), tile t0 + k nw: the per-slot tile sums
+  // are then one plain store per tile (lane k: slot k), no atomics. kTileShift = 8 (asserted below).
+  static_assert(kTileShift == 8, "4 groups of 64 records per tile");
+  const uint32_t ntiles = (ngroups + 3u) >> 2;
   const uint32_t nw = gridDim.x * kWaves;
-  uint32_t g = blockIdx.x * kWaves + wib;
-  // the next group's offsets are requested before this group's window loads (they return together)
-  uint64_t nst = 0, nen = 0;
-  if (g < ngroups && (g << 6) + lane < B.n) {
-    nst = B.start[(g << 6) + lane];
-    nen = B.end[(g << 6) + lane];
-  }
-  for (; g < ngroups; g += nw) {
+  const uint32_t t0 = blockIdx.x * kWaves + wib;
+  if (t0 >= ntiles) return;  // (wave-uniform; no barrier follows)
+  // the group after g in this wave's sequence: the next of its tile, else the next tile's first
+  auto nxt = [&](uint32_t gg) -> uint32_t {
+    return ((gg & 3u) != 3u && gg + 1u < ngroups) ? gg + 1u : 4u * ((gg >> 2) + nw);
+  };
+  uint32_t g = 4u * t0;
+  // Software pipeline, one group deep: group g's window is loaded during the group before it and
+  // the offsets of the group after it during it, both BEFORE the column stores of the group before.
+  // (gfx9 counts stores in vmcnt, in issue order: a load issued after a group's stores could only be
+  // waited for together with them, i.e. every group would wait out its predecessor's store round
+  // trip.)
+  auto offsets = [&](uint32_t gg, uint64_t& s, uint64_t& e) {
+    s = 0;
+    e = 0;
+    if (gg < ngroups && (gg << 6) + lane < B.n) {
+      s = B.start[(gg << 6) + lane];
+      e = B.end[(gg << 6) + lane];
+    }
+  };
+  auto in_batch = [&](uint32_t gg, uint64_t s, uint64_t e) {
+    return gg < ngroups && (gg << 6) + lane < B.n && s <= e && e <= B.nbytes && e >= 4u * W;
+  };
+  uint32_t wn[W];
+  auto window = [&](bool inb, uint64_t e) {
+    const uint32_t voff = inb ? (uint32_t)e - 4u * W : 0xffffff00u;
+#pragma unroll
+    for (int q = 0; q < W / 4; ++q) {
+      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0));
+      wn[4 * q] = v.x;
+      wn[4 * q + 1] = v.y;
+      wn[4 * q + 2] = v.z;
+      wn[4 * q + 3] = v.w;
+    }
+  };
+  uint64_t st, en, nst, nen;
+  offsets(g, st, en);
+  window(in_batch(g, st, en), en);
+  uint32_t g1 = nxt(g);
+  offsets(g1, nst, nen);
+  uint32_t acc = 0;  // lane k: slot k's value count over this tile's records so far
+  while (g < ngroups) {
     const uint32_t r = (g << 6) + lane;
     const bool valid = r < B.n;
-    const uint64_t st = nst, en = nen;
-    const uint32_t gn = g + nw;
-    if (gn < ngroups && (gn << 6) + lane < B.n) {
-      nst = B.start[(gn << 6) + lane];
-      nen = B.end[(gn << 6) + lane];
-    }
-    const bool inb = valid && st <= en && en <= B.nbytes && en >= 4u * W;
+    const bool inb = in_batch(g, st, en);
     const uint32_t en32 = (uint32_t)en;
     const uint32_t voff = inb ? en32 - 4u * W : 0xffffff00u;
     const uint32_t rl = (uint32_t)(en - st);
     uint32_t w[W];
 #pragma unroll
-    for (int q = 0; q < W / 4; ++q) {
-      const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0));
-      w[4 * q] = v.x;
-      w[4 * q + 1] = v.y;
-      w[4 * q + 2] = v.z;
-      w[4 * q + 3] = v.w;
-    }
+    for (int i = 0; i < W; ++i) w[i] = wn[i];
+    // the next group's window, then the offsets of the one after it
+    const uint32_t gn = g1;
+    window(in_batch(gn, nst, nen), nen);
+    st = nst;
+    en = nen;
+    g1 = nxt(gn);
+    offsets(g1, nst, nen);
     bool hit = false;
-    const uint32_t tile = g >> (kTileShift - 6);
     for (uint32_t t = 0; t < A.n_tpl; ++t) {  // (wave-uniform)
       cu32* tp = (cu32*)tpl + t * kLtWords;
       const uint32_t L = tp[kLtL];
@@ -168,8 +200,17 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
         const uint32_t slot = e0 & 0xffu, mode = (e0 >> 8) & 0xfu, len = e0 >> 16;
         const LeanTgt& T = A.tg[slot];
         uint32_t lx, ly = 0;
-        if (mode == 1u || mode == 2u) {  // one int64 varint / one float: 4 bytes at window byte pos (L1 hit)
-          const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, voff, pos, 0);
+        if (mode == 1u || mode == 2u) {  // one int64 varint / one float: the 4 bytes at window byte pos
+          // (from the window's registers: a load here would wait out every store before it, vmcnt)
+          const uint32_t q = pos >> 2;
+          uint32_t a = 0, b = 0;
+#pragma unroll
+          for (int i = 0; i < W; ++i)
+            if (q == (uint32_t)i) {  // (wave-uniform)
+              a = w[i];
+              b = i + 1 < W ? w[i + 1] : 0u;
+            }
+          const uint32_t x = __builtin_amdgcn_alignbyte(b, a, pos & 3u);
           lx = mode == 1u ? vgroups(x, bytes_mask(len)) : x;
         } else if (mode == 3u) {  // one bytes element: its batch offset and length
           lx = en32 + pos;
@@ -195,8 +236,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
             T.loc[r] = make_uint2(lx, ly);
           }
         }
-        const uint32_t cv = cw & ~kCountInline;
-        if (cv && lane == 0) atomicAdd(A.tsum + T.tsum + tile, cv * hits);
+        acc += lane == slot ? (cw & ~kCountInline) * hits : 0u;
       }
       for (uint32_t m = tp[kLtAbsent]; m; m &= m - 1u) {  // slots the shape lacks: order / count 0
         const LeanTgt& T = A.tg[__builtin_ctz(m)];
@@ -212,6 +252,13 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
       o.lmask[g] = mm;
       if (mm) o.rlist[atomicAdd(&o.info[kInfoResid], 1u)] = g;
     }
+    // the tile's sums: the first writer of tsum (zero before the decode; k_lane_count's residual
+    // records add theirs with atomics after this kernel)
+    if ((g & 3u) == 3u || g + 1u >= ngroups) {
+      if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + (g >> 2)] = acc;
+      acc = 0;
+    }
+    g = gn;
   }
 }
 
@@ -220,7 +267,8 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
 hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* tpl, uint32_t w,
                            const uint32_t* d_tab, int num_cus, hipStream_t st) {
   const uint32_t groups = (b.n + 63u) / 64u;
-  const uint32_t need = (groups + kTplBlock / 64 - 1) / (kTplBlock / 64);
+  const uint32_t tiles = (groups + 3u) / 4u;  // (one wave per 256-record tile)
+  const uint32_t need = (tiles + kTplBlock / 64 - 1) / (kTplBlock / 64);
   const uint32_t per_cu = w == 16 ? 4u : (w == 32 ? 2u : 1u);  // (the launch bounds' waves per SIMD)
   const uint32_t resident = per_cu * (uint32_t)num_cus;
   const dim3 grid(need < resident ? (need ? need : 1u) : resident);
