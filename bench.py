@@ -331,7 +331,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         # out-of-line lists: every value written once (their record bytes are counted by the lanes)
-        "k_list_gather": vals,
+        "k_tail_gather": vals,
     }
     a_bytes = alg.get(dominant, framed + 20 * n)
     launches = len(plan)

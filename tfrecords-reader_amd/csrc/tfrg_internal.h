@@ -124,7 +124,7 @@ enum InfoIdx : uint32_t {
   kInfoHuge = 6,         // wave records too large for the LDS stage (listed from the end of big_list)
   kInfoSlow = 7,         // lane records left to the exact (slow) walker
   kInfoSpineDone = 8,    // spine workgroups finished (the last one computes the column bases)
-  kInfoNeed = 9,         // lane records with an out-of-line list (k_list_gather; listed in slow_list)
+  kInfoNeed = 9,         // lane records with an out-of-line list (k_tail_gather; listed in slow_list)
   kInfoSpineTicket = 10, // k_spine workgroup tickets (chunk order of the look-back)
   kInfoOverflow = 11,    // a kind's value total exceeds its column capacity (overlapping ranges)
   kInfoBytesTicket = 12, // k_bytes_scan tile tickets
@@ -132,7 +132,8 @@ enum InfoIdx : uint32_t {
   kInfoCrcCtr = 14,      // [14..15] u64: streaming-CRC list entries << kCrcIdxShift | flat 1 KiB rounds
   kInfoDefer = 16,       // k_lane_count: 64-record rows of deferred packed-int64 bodies reserved (k_body_count)
   kInfoResid = 17,       // k_tpl_lane: 64-record groups listed for k_lane_count (records no template took)
-  kInfoGatherDone = 18,  // k_list_gather workgroups finished (the last one clears irr for the next decode)
+  kInfoPlacedLo = 18,    // [18..19] k_down_gather: the (first 64) slots whose speculative placement is final
+  kInfoPlacedHi = 19,
   kInfoCount = 20
 };
 
@@ -183,12 +184,12 @@ struct DevOut {
                          // prefix (flag 1 / 2; zeroed per decode with tsum)
   uint32_t n_chunks;     // ceil(n_tiles / 2^kSpineChunkShift)
   uint32_t* slow_list;   // [n] lane records for the exact walker; reused by k_down_gather for the
-                         // records k_list_gather decodes (the slow list is consumed by then)
+                         // records k_tail_gather decodes (the slow list is consumed by then)
   uint32_t* crc_rec;     // [n] streaming-CRC list: record
   uint64_t* crc_base;    // [n] its first flat round (ascending with the list index)
   uint64_t* crc_part;    // [n] rounds done << 32 | XOR of the slices, of a record split over waves
   uint32_t* irr;         // [n_slots] records not placed speculatively per slot (DevSchema::spec; after
-                         // the scan words in their buffer, zero between decodes: k_list_gather clears)
+                         // the scan words in their buffer, zero between decodes: k_tail_gather clears)
   uint4* dq;             // [dq_blocks][64][kDeferK] deferred bodies (nullptr: no deferral this decode)
   uint8_t* dq_cnt;       // [dq_blocks][64] entries used per row (0 for records not accepted)
   uint32_t dq_blocks;
@@ -244,7 +245,7 @@ struct LaunchCfg {
 
 // Kernel stages, in launch order (profiling events bracket each one).
 enum Stage : int { kStageTplLane = 0, kStageLaneCount, kStageBodyCount, kStageTailCount, kStageSpine,
-                   kStageDownGather, kStageListGather, kStageMaterialize, kNumStages };
+                   kStageDownGather, kStageTailGather, kStageMaterialize, kNumStages };
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.

@@ -2572,8 +2572,9 @@ __device__ __forceinline__ bool fast_list_gather(const FastSrc& s, const DevOut&
 // caller's first pass)
 template <bool COMPAT, class S>
 __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t r,
-                                              S& s) {
+                                              S& s, uint64_t placed) {
   for (uint32_t k = 0; k < sc.n_slots; ++k) {
+    if (k < 64u && ((placed >> k) & 1ull)) continue;  // (count words of k_tpl_lane records unwritten)
     const size_t at = (size_t)k * B.n + r;
     const uint32_t c = o.count[at];
     if (!c || (c & kCountInline)) continue;
@@ -2610,6 +2611,10 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
     for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;
   pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) |
           __builtin_amdgcn_readfirstlane((uint32_t)pmask);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // (for k_tail_gather, which clears irr)
+    o.info[kInfoPlacedLo] = (uint32_t)pmask;
+    o.info[kInfoPlacedHi] = (uint32_t)(pmask >> 32);
+  }
   auto placed = [&](uint32_t k) -> bool {
     return k < 64u ? ((pmask >> k) & 1ull) != 0ull : k < S && spec_placed(sc.spec, o, k);
   };
@@ -2722,7 +2727,7 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
 // of a wave are usually one contiguous span): staged in LDS and decoded by their own lane.
 template <bool COMPAT>
 __device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint32_t lane_max,
-                                 uint8_t* stage) {
+                                 uint8_t* stage, uint64_t placed) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nneed = o.info[kInfoNeed];
   const uint32_t S = sc.n_slots;
@@ -2749,6 +2754,7 @@ __device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const D
         LdsSrc s;
         s.init(stage, lo16, v.p0, v.L);
         for (uint32_t k = 0; k < S; ++k) {
+          if (k < 64u && ((placed >> k) & 1ull)) continue;  // (count words of k_tpl_lane records unwritten)
           const size_t at = (size_t)k * B.n + r;
           const uint32_t c = o.count[at];
           if (!c || (c & kCountInline)) continue;
@@ -2761,7 +2767,7 @@ __device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const D
       } else {
         Src s;
         s.init(B.bytes, v.p0, v.L);
-        gather_record<COMPAT>(B, sc, o, r, s);
+        gather_record<COMPAT>(B, sc, o, r, s, placed);
       }
     }
     wave_lds_sync();
@@ -2770,7 +2776,7 @@ __device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const D
 
 // Huge records: one slot per lane, lists read from HBM.
 template <bool COMPAT>
-__device__ void role_wave_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o) {
+__device__ void role_wave_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint64_t placed) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nhuge = o.info[kInfoHuge];
   for (uint32_t i = blockIdx.x * kWavesPerBlock + wib; i < nhuge; i += gridDim.x * kWavesPerBlock) {
@@ -2778,6 +2784,7 @@ __device__ void role_wave_gather(const DevBatch& B, const DevSchema& sc, const D
     if (o.status[r] != TFRG_OK) continue;  // wave-uniform
     const RecView v = rec_view(B, r);
     for (uint32_t k = lane; k < sc.n_slots; k += 64) {
+      if (k < 64u && ((placed >> k) & 1ull)) continue;  // (count words of k_tpl_lane records unwritten)
       const size_t at = (size_t)k * B.n + r;
       const uint32_t c = o.count[at];
       if (!c || (c & kCountInline)) continue;  // absent / empty, or written inline by k_down_gather
@@ -2823,14 +2830,11 @@ __device__ __forceinline__ uint32_t count_terms(const uint8_t* l, uint32_t base,
   return n;
 }
 
-// One varint of 1..10 bytes at payload offset `pos`, branch-free: four aligned dwords give the 12
-// bytes at pos, per-word masks of the bytes up to the first terminator give its length (popcount),
-// the 7-bit groups of each word are compacted under those masks and combined
-// (COMPAT: the reference's int-width shifts, decoder.pyx:34-50, as in fast_value). The caller
-// guarantees a terminator before the end of the body (its last byte is one), so the bytes read past
-// it never matter. false = more than 10 bytes (the exact path reports it).
-// The varint whose first byte is the low byte of w0 (w0, w1, w2: the 12 bytes from there): its
-// value and length in bytes, 0 = more than 10 bytes.
+// The varint whose first byte is the low byte of w0 (w0, w1, w2: the 12 bytes from there),
+// branch-free: per-word masks of the bytes up to the first terminator (t ^ (t - 1): all ones when
+// the word has none; zero past the terminator's word) give its length (popcount), the 7-bit groups
+// of each word are compacted under those masks and combined (COMPAT: the reference's int-width
+// shifts, decoder.pyx:34-50, as in fast_value). Returns the length in bytes, 0 = more than 10.
 template <bool COMPAT>
 __device__ __forceinline__ uint32_t varint_w(uint32_t w0, uint32_t w1, uint32_t w2, int64_t& val) {
   const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
@@ -2849,31 +2853,26 @@ __device__ __forceinline__ uint32_t varint_w(uint32_t w0, uint32_t w1, uint32_t 
   return (t0 | t1 | t2) != 0u ? nb : 0u;
 }
 
+// the 12 stage bytes at offset `off` as three words (four aligned dwords: two ds_read2 from one address)
+__device__ __forceinline__ void stage_w3(const uint8_t* l, uint32_t off, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+  const uint32_t sh = off & 3u;
+  const uint32_t* W = reinterpret_cast<const uint32_t*>(l) + (off >> 2);
+  const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
+  w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+  w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+}
+
+// One varint of 1..10 bytes at payload offset `pos` of a staged record. The caller guarantees a
+// terminator before the end of the body (its last byte is one), so the bytes read past it never
+// matter. false = more than 10 bytes (the exact path reports it).
 template <bool COMPAT>
 __device__ __forceinline__ bool varint_bf(const FastSrc& s, uint32_t& pos, int64_t& val) {
-  // four aligned dwords (two ds_read2 from one address) -> the 12 bytes at pos
-  const uint32_t off = s.p + pos, sh = off & 3u;
-  const uint32_t* W = reinterpret_cast<const uint32_t*>(s.l) + (off >> 2);
-  const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
-  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-  const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
-  // per word, the bits of the bytes up to and including the first terminator (t ^ (t - 1): all
-  // ones when the word has none; zero past the terminator's word) -- selects, no branches
-  const uint32_t m0 = t0 ^ (t0 - 1u);
-  const uint32_t m1 = t0 ? 0u : t1 ^ (t1 - 1u);
-  const uint32_t m2 = (t0 | t1) ? 0u : (t2 ^ (t2 - 1u)) & 0xffffu;
-  const uint32_t nb = (uint32_t)(__popc(m0) + __popc(m1) + __popc(m2)) >> 3;
-  const uint32_t x = vgroups(w0, m0), x1 = vgroups(w1, m1), x2 = vgroups(w2, m2);  // groups 0-3, 4-7, 8-9
+  uint32_t w0, w1, w2;
+  stage_w3(s.l, s.p + pos, w0, w1, w2);
+  const uint32_t nb = varint_w<COMPAT>(w0, w1, w2, val);
   pos += nb;
-  if (COMPAT) {
-    const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
-    const bool neg = ((x1 >> 3) | (x2 >> 7)) & 1u;
-    val = (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
-  } else {
-    val = (int64_t)((uint64_t)x | ((uint64_t)x1 << 28) | ((uint64_t)x2 << 56));
-  }
-  return (t0 | t1 | t2) != 0u;  // else more than 10 bytes
+  return nb != 0u;
 }
 
 // Canonical packed int64 lists of one staged record, balanced over the whole wave. The bodies of
@@ -2959,26 +2958,14 @@ __device__ __forceinline__ bool int64_balanced(const FastSrc& fs, const DevOut& 
 }
 
 // One varint at stage offset s whose length the caller has checked (1..10 bytes, its first byte
-// < 0x80 is its last): byte masks from the terminator bits, the reference's compat shifts as
-// varint_bf (decoder.pyx:34-50).
+// < 0x80 is its last)
 template <bool COMPAT>
 __device__ __forceinline__ int64_t varint_term(const uint8_t* l, uint32_t s) {
-  const uint32_t sh = s & 3u;
-  const uint32_t* W = reinterpret_cast<const uint32_t*>(l) + (s >> 2);
-  const uint32_t d0 = W[0], d1 = W[1], d2 = W[2], d3 = W[3];
-  const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh), w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-  const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-  const uint32_t t0 = ~w0 & 0x80808080u, t1 = ~w1 & 0x80808080u, t2 = ~w2 & 0x00008080u;
-  const uint32_t m0 = t0 ^ (t0 - 1u);
-  const uint32_t m1 = t0 ? 0u : t1 ^ (t1 - 1u);
-  const uint32_t m2 = (t0 | t1) ? 0u : (t2 ^ (t2 - 1u)) & 0xffffu;
-  const uint32_t x = vgroups(w0, m0), x1 = vgroups(w1, m1), x2 = vgroups(w2, m2);
-  if (COMPAT) {
-    const uint32_t lo32 = x | (x1 << 28) | ((x1 >> 7) << 3) | (x2 << 24);
-    const bool neg = ((x1 >> 3) | (x2 >> 7)) & 1u;
-    return (int64_t)(((uint64_t)(neg ? 0xffffffffu : 0u) << 32) | lo32);
-  }
-  return (int64_t)((uint64_t)x | ((uint64_t)x1 << 28) | ((uint64_t)x2 << 56));
+  uint32_t w0, w1, w2;
+  stage_w3(l, s, w0, w1, w2);
+  int64_t v;
+  (void)varint_w<COMPAT>(w0, w1, w2, v);
+  return v;
 }
 
 // Canonical packed int64 lists of one staged record, value-parallel with COALESCED stores. In
@@ -3148,7 +3135,7 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
 // while this one is gathered (48 VGPRs live across the gather).
 template <bool COMPAT>
 __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage,
-                                  uint16_t* ring) {
+                                  uint16_t* ring, uint64_t placed) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t nbig = o.info[kInfoBig];
   if (blockIdx.x * kWavesPerBlock + wib >= nbig) return;  // wave-uniform: no records for this wave
@@ -3167,7 +3154,8 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
   q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
   // per-slot constants, and the slot metadata of the NEXT record loaded one record ahead (its
   // latency then hides behind this record's gather instead of opening every record)
-  const bool sl = lane < sc.n_slots;
+  // (slots placed by k_tpl_lane: their count words are unwritten for its records)
+  const bool sl = lane < sc.n_slots && !((placed >> lane) & 1ull);
   const uint32_t kind_l = sl ? (uint32_t)sc.slot_kind[lane] : 0u;
   const uint64_t sbase_l = sl ? o.slot_base[lane] : 0ull;
   uint32_t c_n = 0, rs_n = 0;
@@ -3246,132 +3234,11 @@ __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchem
   uint16_t* ring = reinterpret_cast<uint16_t*>(stage + kWStageStride);  // (int64_ring)
   if (blockIdx.x == 0)  // (read by k_down_gather, which has finished: zero for the next decode)
     for (uint32_t k = threadIdx.x; k < sc.n_slots; k += kWaveBlock) o.irr[k] = 0u;
-  role_list_gather<COMPAT>(B, sc, o, lane_max, stage);
-  role_stage_gather<COMPAT>(B, sc, o, stage, ring);
-  role_wave_gather<COMPAT>(B, sc, o);
-}
-
-// ------------------------------------------------------------------------------------------------
-// List gather: every out-of-line list of the batch, ONE LANE per (record, slot) list, straight from
-// HBM. k_down_gather listed the records with such lists (kInfoNeed entries of slow_list, tile order:
-// a wave's 64 records are usually consecutive). A workgroup takes 64 of them, its wave w the slots
-// w, w + 8, ...: for one slot the 64 lanes read their own records' bodies and write their own ranges
-// of the slot's column (the wave's stores cover one contiguous region of the column: lists of
-// consecutive records are adjacent). Canonical packed lists (one chunk, tag 0x0a, as the count pass
-// accepted them) take the fast forms: int64 one 16-byte load per value at the value's first byte
-// (varint_w), float 16-byte copies; anything else the exact list walk (list_values, decoder.pyx:
-// 235-300). No LDS, no record staging: every wave keeps 64 independent chains of loads in flight.
-// ------------------------------------------------------------------------------------------------
-constexpr int kListBlock = 512;
-typedef uint32_t lg_u32x4 __attribute__((ext_vector_type(4)));
-
-// the c values of a canonical packed int64 body at absolute bytes [bo, bo + bl) into out[0, c);
-// false = a varint of more than 10 bytes or a body that does not end on the c-th value (the
-// caller's exact walk then rewrites the whole range)
-template <bool COMPAT>
-__device__ __forceinline__ bool lane_i64(__amdgpu_buffer_rsrc_t in, uint32_t bo, uint32_t bl, uint32_t c,
-                                         int64_t* out) {
-  uint32_t pos = bo;
-  bool ok = true;
-  for (uint32_t j = 0; j < c; ++j) {
-    const lg_u32x4 w = __builtin_bit_cast(lg_u32x4, __builtin_amdgcn_raw_buffer_load_b128(in, pos, 0, 0));
-    int64_t v;
-    const uint32_t nb = varint_w<COMPAT>(w.x, w.y, w.z, v);
-    ok &= nb != 0u;
-    pos += nb ? nb : 1u;
-    out[j] = v;
-  }
-  return ok && pos == bo + bl;
-}
-
-// the c floats of a canonical packed float body at absolute byte bo into out[0, c)
-__device__ __forceinline__ void lane_f32(__amdgpu_buffer_rsrc_t in, uint32_t bo, uint32_t c, uint32_t* out) {
-  uint32_t j = 0;
-  for (; j + 4u <= c; j += 4u) {
-    const uint4 x = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(in, bo + 4u * j, 0, 0));
-    *reinterpret_cast<uint4*>(out + j) = x;
-  }
-  for (; j < c; ++j) out[j] = __builtin_amdgcn_raw_buffer_load_b32(in, bo + 4u * j, 0, 0);
-}
-
-template <bool COMPAT>
-__global__ __launch_bounds__(kListBlock) void k_list_gather(DevBatch B, DevSchema sc, DevOut o) {
-  constexpr uint32_t kW = kListBlock / 64;
-  const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t S = sc.n_slots;
-  const uint32_t nneed = o.info[kInfoNeed];
-  if (!nneed) {  // (grid-uniform) nothing to gather: irr is read by no workgroup, cleared by one
-    if (blockIdx.x == 0)
-      for (uint32_t k = threadIdx.x; k < S; k += kListBlock) o.irr[k] = 0u;
-    return;
-  }
-  // slots whose speculative placement is final: nothing to gather (their count words may not be
-  // written at all: k_tpl_lane). irr is read here and cleared by the last workgroup.
-  uint64_t pmask = 0;
-  if (sc.spec)
-    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;
-  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)pmask);
-  // (batches of 4 GiB and more take the exact walk: 32-bit buffer offsets)
-  const bool fast = B.nbytes < 0xffffff00ull;
-  const __amdgpu_buffer_rsrc_t in =
-      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B.bytes), (short)0, fast ? (int)(uint32_t)B.nbytes : 0,
-                                        0x00020000);
-  for (uint32_t base = blockIdx.x * 64u; base < nneed; base += gridDim.x * 64u) {  // (workgroup-uniform)
-    const uint32_t i = base + lane;
-    const bool rin = i < nneed;
-    const uint32_t r = rin ? o.slow_list[i] : 0u;
-    const RecView v = rec_view(B, r);
-    for (uint32_t k = wib; k < S; k += kW) {  // (wave-uniform)
-      if (k < 64u ? ((pmask >> k) & 1ull) != 0ull : (sc.spec && spec_placed(sc.spec, o, k))) continue;
-      const size_t at = (size_t)k * B.n + r;
-      const uint32_t c = rin ? o.count[at] : 0u;
-      const bool ool = c != 0u && !(c & kCountInline);
-      if (!__ballot(ool)) continue;
-      uint2 lc = make_uint2(0, 0);
-      uint64_t dst = 0;
-      if (ool) {
-        lc = o.loc[at];
-        dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
-      }
-      const uint32_t kind = sc.slot_kind[k];
-      bool done = !ool;
-      if (fast && ool && kind != TFRG_KIND_BYTES) {
-        // the list's one canonical chunk: tag 0x0a, length varint of <= 3 bytes, body to the list's end
-        const uint32_t hp = (uint32_t)(v.p0 + lc.x);
-        const uint32_t w = __builtin_amdgcn_raw_buffer_load_b32(in, hp, 0, 0);
-        const uint32_t b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu, b3 = w >> 24;
-        const uint32_t h = b1 < 0x80u ? 2u : b2 < 0x80u ? 3u : 4u;
-        const uint32_t bl = (b1 & 0x7fu) | (h > 2u ? (b2 & 0x7fu) << 7 : 0u) | (h > 3u ? (b3 & 0x7fu) << 14 : 0u);
-        bool ok = (w & 0xffu) == 0x0au && (h < 4u || b3 < 0x80u) && lc.y >= h && bl == lc.y - h;
-        if (kind == TFRG_KIND_INT64) {
-          ok &= dst + c <= o.cap_i64;
-          if (ok) done = lane_i64<COMPAT>(in, hp + h, bl, c, o.i64 + dst);
-        } else {
-          ok &= bl == 4u * c && dst + c <= o.cap_f32;
-          if (ok) {
-            lane_f32(in, hp + h, c, o.f32 + dst);
-            done = true;
-          }
-        }
-      }
-      if (!done) {  // anything else: the exact list walk (a failed fast form is rewritten whole)
-        Src s;
-        s.init(B.bytes, v.p0, v.L);
-        list_gather<COMPAT>(s, o, (int)kind, (int64_t)lc.x, (int64_t)lc.y, dst);
-      }
-    }
-  }
-  // the last workgroup to finish clears irr (read above by every workgroup) for the next decode
-  __shared__ uint32_t s_last;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    s_last = atomicAdd(&o.info[kInfoGatherDone], 1u) == gridDim.x - 1u;
-  }
-  __syncthreads();
-  if (s_last)
-    for (uint32_t k = threadIdx.x; k < S; k += kListBlock) o.irr[k] = 0u;
+  // the slots whose speculative placement is final (k_down_gather's mask; irr is cleared above)
+  const uint64_t placed = ((uint64_t)o.info[kInfoPlacedHi] << 32) | o.info[kInfoPlacedLo];
+  role_list_gather<COMPAT>(B, sc, o, lane_max, stage, placed);
+  role_stage_gather<COMPAT>(B, sc, o, stage, ring, placed);
+  role_wave_gather<COMPAT>(B, sc, o, placed);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3382,7 +3249,7 @@ constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (s
 constexpr size_t kLaneLdsBudget = 64 * 1024; // lane kernels (occupancy): likewise
 
 const char* const kStageNames[kNumStages] = {"k_tpl_lane",    "k_lane_count",  "k_body_count", "k_tail_count", "k_spine",
-                                             "k_down_gather", "k_list_gather", "k_bytes"};
+                                             "k_down_gather", "k_tail_gather", "k_bytes"};
 
 static inline size_t r16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -3515,25 +3382,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                          0, st, b, scx, ox, cfg.lane_max, n_tiles);
     }
   }
-  mark(kStageListGather);
-  if (S > 0) {  // the out-of-line lists of every record, one lane per list
-#ifdef TFRG_STAGE_GATHER  // (measurement build only: the round-3 staged gather)
+  mark(kStageTailGather);
+  if (S > 0) {  // the gathers after the scan: lane records' lists, staged and huge large records
     const size_t lds = (size_t)kWRegion * kWavesPerBlock;
     const void* fn = reinterpret_cast<const void*>(&k_tail_gather<COMPAT>);
-    int per_cu = 0;
+    int per_cu = 0;  // one round of resident workgroups (3 per CU: a second round would run at 1/3)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
     hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, ox, cfg.lane_max);
-#else
-    const void* fn = reinterpret_cast<const void*>(&k_list_gather<COMPAT>);
-    int per_cu = 0;  // one round of resident workgroups, striding over the listed records
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kListBlock, 0) != hipSuccess || per_cu < 1)
-      per_cu = 1;
-    const uint32_t need_max = (b.n + 63u) / 64u;  // (the listed records are at most the batch)
-    const uint32_t g = std::min<uint32_t>(std::max<uint32_t>(need_max, 1u), (uint32_t)(per_cu * cfg.num_cus));
-    hipLaunchKernelGGL((k_list_gather<COMPAT>), dim3(g), dim3(kListBlock), 0, st, b, scx, ox);
-#endif
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)
   return hipGetLastError();

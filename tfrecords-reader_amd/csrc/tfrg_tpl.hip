@@ -15,9 +15,9 @@
 //     32 bytes from the end first run a slice-by-4 chain whose state joins at distance 28..31;
 //   * the template's dict straight into the columns: order, count / loc, or the speculatively
 //     placed value + row split (DevSchema::spec), and the per-tile value counts.
-// A record no template takes (another shape, a framing or CRC mismatch, a record at the very start
-// of the batch whose window would begin before it) is left to k_lane_count: per 64-record group a
-// miss mask (DevOut::lmask) and a list of the groups with misses (DevOut::rlist).
+// A record no template takes (another shape, a framing or CRC mismatch) is left to k_lane_count:
+// per 64-record group a miss mask (DevOut::lmask) and a list of the groups with misses
+// (DevOut::rlist).
 #include <hip/hip_runtime.h>
 #include "tfrg_internal.h"
 #include "crc32c.h"
@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t bytes_mask(uint32_t nb) { return nb >= 4u ? 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 template <int W>
-__global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_tpl_lane(
+__global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_tpl_lane(
     DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ tpl, const uint32_t* __restrict__ tabs) {
   static_assert(W == 16 || W == 32 || W == 64, "window words");
   __shared__ uint32_t tab[kTplTabs * 256];
@@ -101,16 +101,10 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
   const uint32_t nw = gridDim.x * kWaves;
   const uint32_t t0 = blockIdx.x * kWaves + wib;
   if (t0 >= ntiles) return;  // (wave-uniform; no barrier follows)
-  // the group after g in this wave's sequence: the next of its tile, else the next tile's first
-  auto nxt = [&](uint32_t gg) -> uint32_t {
-    return ((gg & 3u) != 3u && gg + 1u < ngroups) ? gg + 1u : 4u * ((gg >> 2) + nw);
-  };
-  uint32_t g = 4u * t0;
-  // Software pipeline, one group deep: group g's window is loaded during the group before it and
-  // the offsets of the group after it during it, both BEFORE the column stores of the group before.
-  // (gfx9 counts stores in vmcnt, in issue order: a load issued after a group's stores could only be
-  // waited for together with them, i.e. every group would wait out its predecessor's store round
-  // trip.)
+  // Two groups per step (g, g + 1 of the wave's tile), their windows loaded together: a step waits
+  // once, for both windows and the previous step's column stores (gfx9 counts stores in vmcnt, in
+  // issue order), so each wait covers 128 records. The offsets of the next step are requested
+  // before this step's stores (they are then ready without waiting for those).
   auto offsets = [&](uint32_t gg, uint64_t& s, uint64_t& e) {
     s = 0;
     e = 0;
@@ -120,11 +114,11 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
     }
   };
   auto in_batch = [&](uint32_t gg, uint64_t s, uint64_t e) {
-    return gg < ngroups && (gg << 6) + lane < B.n && s <= e && e <= B.nbytes && e >= 4u * W;
+    return gg < ngroups && (gg << 6) + lane < B.n && s <= e && e <= B.nbytes && e >= 16u;
   };
-  uint32_t wn[W];
-  auto window = [&](bool inb, uint64_t e) {
-    const uint32_t voff = inb ? (uint32_t)e - 4u * W : 0xffffff00u;
+  auto window = [&](uint32_t (&wn)[W], bool inb, uint64_t e, uint32_t gg) {
+    const bool full = inb && e >= 4u * W;
+    const uint32_t voff = full ? (uint32_t)e - 4u * W : 0xffffff00u;
 #pragma unroll
     for (int q = 0; q < W / 4; ++q) {
       const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0));
@@ -133,30 +127,30 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
       wn[4 * q + 2] = v.z;
       wn[4 * q + 3] = v.w;
     }
+    // a record ending in the batch's first 4 W bytes (group 0 only): its window begins before the
+    // batch; those bytes are outside the record (template mask 0), the rest is read byte by byte
+    const bool head = inb && !full;
+    if (gg == 0u && __ballot(head)) {
+#pragma unroll
+      for (int i = 0; i < W; ++i) {
+        uint32_t x = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int64_t p = (int64_t)e - 4 * W + 4 * i + b;
+          if (head && p >= 0) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0) << (8 * b);
+        }
+        if (head) wn[i] = x;
+      }
+    }
   };
-  uint64_t st, en, nst, nen;
-  offsets(g, st, en);
-  window(in_batch(g, st, en), en);
-  uint32_t g1 = nxt(g);
-  offsets(g1, nst, nen);
   uint32_t acc = 0;  // lane k: slot k's value count over this tile's records so far
-  while (g < ngroups) {
+  // one group: template match + CRC, the template's dict into the columns, the miss mask
+  auto proc = [&](const uint32_t (&w)[W], uint32_t g, uint64_t st, uint64_t en) {
     const uint32_t r = (g << 6) + lane;
     const bool valid = r < B.n;
     const bool inb = in_batch(g, st, en);
     const uint32_t en32 = (uint32_t)en;
-    const uint32_t voff = inb ? en32 - 4u * W : 0xffffff00u;
     const uint32_t rl = (uint32_t)(en - st);
-    uint32_t w[W];
-#pragma unroll
-    for (int i = 0; i < W; ++i) w[i] = wn[i];
-    // the next group's window, then the offsets of the one after it
-    const uint32_t gn = g1;
-    window(in_batch(gn, nst, nen), nen);
-    st = nst;
-    en = nen;
-    g1 = nxt(gn);
-    offsets(g1, nst, nen);
     bool hit = false;
     for (uint32_t t = 0; t < A.n_tpl; ++t) {  // (wave-uniform)
       cu32* tp = (cu32*)tpl + t * kLtWords;
@@ -252,13 +246,33 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2)) void k_
       o.lmask[g] = mm;
       if (mm) o.rlist[atomicAdd(&o.info[kInfoResid], 1u)] = g;
     }
+  };
+  // the wave's steps: tile t0 + k nw, groups (4t, 4t+1), (4t+2, 4t+3)
+  uint32_t t = t0, p = 0;
+  uint64_t s0, e0, s1, e1;
+  offsets(4u * t, s0, e0);
+  offsets(4u * t + 1u, s1, e1);
+  while (t < ntiles) {
+    const uint32_t ga = 4u * t + p, gb = ga + 1u;
+    uint32_t wa[W], wb[W];
+    window(wa, in_batch(ga, s0, e0), e0, ga);
+    window(wb, in_batch(gb, s1, e1), e1, gb);
+    const uint64_t sa = s0, ea = e0, sb = s1, eb = e1;
+    // the next step's offsets
+    const uint32_t tn = p ? t + nw : t, pn = p ^ 2u;
+    offsets(4u * tn + pn, s0, e0);
+    offsets(4u * tn + pn + 1u, s1, e1);
+    proc(wa, ga, sa, ea);
+    if (gb < ngroups) proc(wb, gb, sb, eb);
     // the tile's sums: the first writer of tsum (zero before the decode; k_lane_count's residual
     // records add theirs with atomics after this kernel)
-    if ((g & 3u) == 3u || g + 1u >= ngroups) {
-      if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + (g >> 2)] = acc;
+    if (p || gb + 1u >= ngroups) {
+      if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + t] = acc;
       acc = 0;
     }
-    g = gn;
+    if (gb + 1u >= ngroups) break;
+    t = tn;
+    p = pn;
   }
 }
 
@@ -269,8 +283,12 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   const uint32_t groups = (b.n + 63u) / 64u;
   const uint32_t tiles = (groups + 3u) / 4u;  // (one wave per 256-record tile)
   const uint32_t need = (tiles + kTplBlock / 64 - 1) / (kTplBlock / 64);
-  const uint32_t per_cu = w == 16 ? 4u : (w == 32 ? 2u : 1u);  // (the launch bounds' waves per SIMD)
-  const uint32_t resident = per_cu * (uint32_t)num_cus;
+  const void* fn = w == 16 ? reinterpret_cast<const void*>(&k_tpl_lane<16>)
+                  : w == 32 ? reinterpret_cast<const void*>(&k_tpl_lane<32>)
+                            : reinterpret_cast<const void*>(&k_tpl_lane<64>);
+  int per_cu = 0;  // one round of resident workgroups, striding over the tiles
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTplBlock, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+  const uint32_t resident = (uint32_t)per_cu * (uint32_t)num_cus;
   const dim3 grid(need < resident ? (need ? need : 1u) : resident);
   const uint32_t* tabs = d_tab + kLeanTabOff;
   switch (w) {
