@@ -343,6 +343,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     out = {
         "workload": w.desc,
         "records": n,
+        "tpl_groups_missed": sum(int(i.tpl_groups_missed) for i in infos),
         "framed_bytes": framed,
         "batches": launches,
         "batch_bytes_max": int((plan[:, 3] - plan[:, 2]).max()),
@@ -531,6 +532,7 @@ def run(args) -> None:
             "batches_per_gpu": head["batches"],
             "batch_bytes_max": head["batch_bytes_max"],
             "streams": head["streams"],
+            "tpl_groups_missed": head["tpl_groups_missed"],
         }
         if meta:
             cfg.update(files_total=meta["files_total"], files_per_gpu=meta["files_mine"],

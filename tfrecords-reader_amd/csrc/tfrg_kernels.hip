@@ -2338,19 +2338,30 @@ constexpr int kSpineBlock = 256;
 constexpr int kSpineItems = 16;
 static_assert(kSpineBlock * kSpineItems == (1 << kSpineChunkShift), "one chunk per spine workgroup");
 
-// exclusive prefix of chunk `chunk` from its predecessors' look-back words (lb[0..chunk))
-__device__ __forceinline__ uint32_t spine_look_back(const uint64_t* lb, uint32_t chunk) {
+// exclusive prefix of chunk `chunk` from its predecessors' look-back words (lb[0..chunk)), by one
+// wave: lane l reads predecessor chunk - 1 - l (64 words per round trip, not one), the nearest
+// inclusive prefix (flag 2) ends the sum; a predecessor in range that has not published its total
+// yet (flag 0; it has started: ticket order) makes the wave read the window again
+__device__ __forceinline__ uint32_t spine_look_back(const uint64_t* lb, uint32_t chunk, uint32_t lane) {
   uint32_t excl = 0;
-  for (int64_t j = (int64_t)chunk - 1; j >= 0;) {
-    const uint64_t w = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int64_t base = (int64_t)chunk - 1; base >= 0;) {  // (wave-uniform)
+    const int64_t j = base - (int64_t)lane;
+    const uint64_t w = j >= 0 ? __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : (2ull << 32);  // (before the first chunk: an inclusive prefix of 0)
     const uint32_t flag = (uint32_t)(w >> 32);
-    if (!flag) {  // predecessor still scanning (it has started: ticket order)
+    const uint64_t inc = __ballot(flag == 2u), unset = __ballot(flag == 0u);
+    const uint32_t stop = inc ? (uint32_t)__builtin_ctzll(inc) : 64u;  // lanes [0, stop] are summed
+    const uint64_t range = stop >= 63u ? ~0ull : (2ull << stop) - 1ull;
+    if (unset & range) {
       __builtin_amdgcn_s_sleep(1);
       continue;
     }
-    excl += (uint32_t)w;
-    if (flag == 2u) break;
-    --j;
+    uint32_t v = lane <= stop ? (uint32_t)w : 0u;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v += (uint32_t)__shfl_xor((int)v, m, 64);
+    excl += v;
+    if (stop < 64u) break;
+    base -= 64;
   }
   return excl;
 }
@@ -2437,13 +2448,16 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
     pre += (uint32_t)w < wid ? x : 0u;
     tot += x;
   }
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&lb[chunk], ((uint64_t)(chunk ? 1u : 2u) << 32) | tot, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t excl = spine_look_back(lb, chunk);
-    if (chunk) __hip_atomic_store(&lb[chunk], (2ull << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (chunk == o.n_chunks - 1u) o.totals[slot] = excl + tot;
-    s_excl = excl;
+  if (threadIdx.x < 64u) {  // wave 0
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&lb[chunk], ((uint64_t)(chunk ? 1u : 2u) << 32) | tot, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t excl = spine_look_back(lb, chunk, lane);
+    if (threadIdx.x == 0) {
+      if (chunk) __hip_atomic_store(&lb[chunk], (2ull << 32) | (excl + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (chunk == o.n_chunks - 1u) o.totals[slot] = excl + tot;
+      s_excl = excl;
+    }
   }
   __syncthreads();
   uint32_t run = s_excl + pre + incl - sum;

@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Measurement-only builds of libtfrg (never the product library): the kernel sources copied to a
+temporary directory, patched, built into tfr_reader/libtfrg_<name>.so (load with TFRG_LIB=...), for
+paired A/Bs on the GPU box (tools/ab.sh). Patches are (file, old, new) string replacements; a
+variant whose patch no longer applies is an error.  usage: variants.py name [name ...]"""
+import shutil
+import subprocess
+import sys
+import tempfile
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parents[1]
+CS = REPO / "tfrecords-reader_amd" / "csrc"
+
+VARIANTS = {
+    # k_tpl_lane without its column stores (read side alone; wrong results)
+    "nostore": [("tfrg_tpl.hip", "      if (ok) {\n        o.status[r] = TFRG_OK;",
+                 "      if (ok && A.n_tpl > 99) {\n        o.status[r] = TFRG_OK;"),
+                ("tfrg_tpl.hip", "        if (ok) {\n          T.ord[r] = (uint16_t)rank;",
+                 "        if (ok && A.n_tpl > 99) {\n          T.ord[r] = (uint16_t)rank;")],
+    # k_tpl_lane window loads with the streaming (slc) cache policy
+    "ntload": [("tfrg_tpl.hip", "__builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0)",
+                "__builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 2)")],
+    # k_tpl_lane without the status / verdict stores (wrong results)
+    "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
+}
+
+
+def build(name: str) -> Path:
+    with tempfile.TemporaryDirectory() as td:
+        d = Path(td) / "pkg" / "csrc"  # (the sources include ../../include)
+        shutil.copytree(CS, d, ignore=shutil.ignore_patterns("build*"))
+        (Path(td) / "include").symlink_to(REPO / "include")
+        for f, old, new in VARIANTS[name]:
+            src = (d / f).read_text()
+            assert src.count(old) == 1, (name, f, old[:60])
+            (d / f).write_text(src.replace(old, new))
+        out = REPO / "tfrecords-reader_amd" / "tfr_reader" / f"libtfrg_{name}.so"
+        subprocess.run(["make", "-j8", f"OUT={out}", f"PYMOD={Path(td) / 'unused.so'}", f"{out}"], cwd=d, check=True,
+                       stdout=subprocess.DEVNULL)
+    return out
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:]:
+        print(build(n))
