@@ -95,6 +95,10 @@ struct tfrg_ctx {
   DBuf bdata, boff64, blb, bbig;  // TFRG_FLAG_MATERIALIZE_BYTES
   bool materialized = false;
   bool tsum_dirty = true;  // the scan words must be cleared before the next decode
+  // info words: two slots, decode k using slot k % 2; k_lane_count zeroes the other one for the
+  // next decode (no per-call memset). info_clean: the next slot is known to be zero.
+  uint32_t info_slot = 0;
+  bool info_clean = false;
   // last batch
   uint32_t n = 0;
   uint64_t cap_hint = 0;  // tfrg_decode_host: total bytes of the given ranges (>= nbytes when they overlap)
@@ -732,14 +736,20 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       c->slot_base.ensure((S + 1) * 8) || c->totals.ensure((S + 1) * 4) || c->kind_totals.ensure(32) ||
       c->i64.ensure(cap_i64 * 8) || c->f32.ensure(cap_f32 * 4) || c->b_off.ensure(cap_b * 4) ||
       c->b_len.ensure(cap_b * 4) || c->big_list.ensure(nn * 4) || c->slow_list.ensure(nn * 4) ||
-      c->miss.ensure(kMissCap * 16ull) || c->info.ensure(kInfoCount * 4) ||
+      c->miss.ensure(kMissCap * 16ull) || c->info.ensure(2 * kInfoCount * 4) ||
       c->tsum.ensure(tsum_words * 4 + 16) || c->crc_rec.ensure(nn * 4) || c->crc_base.ensure(nn * 8) ||
       c->crc_part.ensure(nn * 8) || c->lmask.ensure(ngroups * 8) || c->rlist.ensure(ngroups * 4)) {
     set_error("device allocation failed");
     return TFRG_E_NOMEM;
   }
-  // per-call state re-initialised on the stream (Guideline 16: zero every polled word per call)
-  HIP_TRY(hipMemsetAsync(c->info.p, 0, kInfoCount * 4, st));
+  // per-call counters (Guideline 16: every polled word zero per call): this decode's info slot was
+  // zeroed by the previous decode's k_lane_count, else (a fresh context, an empty batch or a failed
+  // launch before) here
+  const uint32_t islot = c->info_slot ^ 1u;
+  uint32_t* const info_cur = c->info.as<uint32_t>() + islot * kInfoCount;
+  if (!c->info_clean) HIP_TRY(hipMemsetAsync(info_cur, 0, kInfoCount * 4, st));
+  c->info_clean = false;
+  c->info_slot = islot;
   // the row-split scan words are zero between decodes (k_down_gather clears what it used): only a
   // fresh buffer, or one a failed launch may have left dirty, is cleared here
   if (c->tsum.cap != tsum_cap0 || c->tsum_dirty) {
@@ -793,7 +803,8 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   o.big_list = c->big_list.as<uint32_t>();
   o.miss = c->miss.as<uint32_t>();
   o.miss_cap = kMissCap;
-  o.info = c->info.as<uint32_t>();
+  o.info = info_cur;
+  o.info_next = c->info.as<uint32_t>() + (islot ^ 1u) * kInfoCount;
   o.tsum = c->tsum.as<uint32_t>();
   o.tile_stride = tile_stride;
   o.spine_lb = reinterpret_cast<uint64_t*>(o.tsum + (size_t)S * tile_stride);  // 16-byte aligned
@@ -876,6 +887,7 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
       return TFRG_E_HIP;
     }
   }
+  c->info_clean = n != 0;  // (k_lane_count ran: the other slot is zero)
   c->n = n;
   c->nbytes = nbytes;
   c->cap_i64 = cap_i64;
@@ -926,7 +938,8 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   HIP_TRY(hipSetDevice(c->device));
   uint32_t h[kInfoCount] = {0};
   uint64_t kt[4] = {0, 0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(h, c->info.p, sizeof(h), hipMemcpyDeviceToHost, c->last_stream));
+  HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, sizeof(h), hipMemcpyDeviceToHost,
+                         c->last_stream));
   HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
   HIP_TRY(hipStreamSynchronize(c->last_stream));
   uint64_t blen = 0;

@@ -113,7 +113,8 @@ struct DevBatch {
   uint32_t flags;
 };
 
-// Info counters (device, zeroed per decode)
+// Info counters (device, zero at the start of every decode: the previous decode's k_lane_count
+// zeroes the slot the next one uses, DevOut::info_next)
 enum InfoIdx : uint32_t {
   kInfoErrors = 0,       // records with a decode error (reference exception / UB status)
   kInfoFirstError = 1,   // ~(lowest record index with an error): atomicMax of ~r, init 0
@@ -178,6 +179,7 @@ struct DevOut {
   uint32_t* miss;        // [miss_cap][4] (record, kind, key abs offset, key length)
   uint32_t miss_cap;
   uint32_t* info;        // [kInfoCount]
+  uint32_t* info_next;   // [kInfoCount] the next decode's info words (k_lane_count workgroup 0 zeroes them)
   uint32_t* tsum;        // [n_slots][tile_stride] per-tile value counts, then their exclusive prefixes
   uint32_t tile_stride;  // >= n_tiles, multiple of 4
   uint64_t* spine_lb;    // [n_slots][n_chunks] k_spine look-back words: flag << 32 | chunk total / inclusive

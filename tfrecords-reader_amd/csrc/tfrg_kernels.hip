@@ -1358,6 +1358,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // residual mode: a workgroup with no listed group exits before loading its tables (block-uniform)
   const bool resid = o.rlist != nullptr;
+  if (blockIdx.x == 0 && threadIdx.x < kInfoCount) o.info_next[threadIdx.x] = 0u;  // (the next decode's)
   const uint32_t nres = resid ? rfl32(o.info[kInfoResid]) : 0u;
   if (resid && blockIdx.x * kWaves >= nres) return;
   uint8_t* stage_all = reinterpret_cast<uint8_t*>(ord) + ord_bytes;

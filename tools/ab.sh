@@ -4,7 +4,7 @@ set -u
 c=$1; shift
 O=gpurun_out/ab; mkdir -p $O
 for L in "$@"; do
-  TFRG_LIB=$PWD/tfrecords-reader_amd/tfr_reader/$L timeout -k 10 200 python bench.py --only "$c" --no-cpu --steps 20 > $O/$L.json 2> $O/$L.err || { tail $O/$L.err; exit 1; }
+  TFRG_LIB=$PWD/tfrecords-reader_amd/tfr_reader/$L timeout -k 10 200 python bench.py --only "$c" --no-cpu --steps ${STEPS:-50} > $O/$L.json 2> $O/$L.err || { tail $O/$L.err; exit 1; }
   python3 - "$O/$L.json" "$L" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

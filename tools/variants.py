@@ -21,6 +21,16 @@ VARIANTS = {
     # k_tpl_lane window loads with the streaming (slc) cache policy
     "ntload": [("tfrg_tpl.hip", "__builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0)",
                 "__builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 2)")],
+    # k_tpl_lane with every valid lane taking template 0 (wrong results; all stores kept)
+    "fakehit": [("tfrg_tpl.hip", "      const bool ok = cand && diff == 0u && crc_mask(lin ^ tp[kLtK]) == w[W - 1];",
+                 "      const bool ok = t == 0u && (diff | lin | 1u) != 0u && (g << 6) + lane < B.n;")],
+    # the same with the window loads made coalesced (lane j: 16 bytes at j * 16 of a 4 KiB span)
+    "fakehit_coal": [("tfrg_tpl.hip", "      const bool ok = cand && diff == 0u && crc_mask(lin ^ tp[kLtK]) == w[W - 1];",
+                      "      const bool ok = t == 0u && (diff | lin | 1u) != 0u && (g << 6) + lane < B.n;"),
+                     ("tfrg_tpl.hip", "    const uint32_t voff = full ? (uint32_t)e - 4u * W : 0xffffff00u;",
+                      "    const uint32_t voff = full ? ((gg * 3712u) & ~15u) + 16u * lane - 48u * lane / 16u * 0u : 0xffffff00u;"),
+                     ("tfrg_tpl.hip", "raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0)",
+                      "raw_buffer_load_b128(rsrc, voff + 1024u * q, 0, 0)")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
