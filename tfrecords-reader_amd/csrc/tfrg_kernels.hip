@@ -2426,6 +2426,14 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
   uint32_t* t = o.tsum + (size_t)slot * o.tile_stride;
   uint64_t* lb = o.spine_lb + (size_t)slot * o.n_chunks;
   const uint32_t i0 = (chunk << kSpineChunkShift) + threadIdx.x * kSpineItems;
+  if (spec_placed(spec, o, slot)) {  // (workgroup-uniform) n values at rows 0..n-1 (spec_failed): no scan
+    // (k_down_gather skips the slot): its tile sums zeroed for the next decode, its look-back words
+    // never written
+#pragma unroll
+    for (int j = 0; j < kSpineItems; j += 4)
+      if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(0, 0, 0, 0);
+    if (chunk == o.n_chunks - 1u && threadIdx.x == 0) o.totals[slot] = n;
+  } else {
   uint32_t v[kSpineItems];
 #pragma unroll
   for (int j = 0; j < kSpineItems; j += 4) {  // tile_stride is a multiple of 4: whole uint4s are in bounds
@@ -2471,6 +2479,7 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
       run += v[j + m];
     }
     if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
   }
   if (threadIdx.x == 0) {
     __threadfence();
@@ -2633,14 +2642,9 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
   auto placed = [&](uint32_t k) -> bool {
     return k < 64u ? ((pmask >> k) & 1ull) != 0ull : k < S && spec_placed(sc.spec, o, k);
   };
-  if (S <= 64u && pmask == (~0ull >> (64u - S))) {  // every slot placed: only the scan words to clear
-    const size_t nz = (size_t)S * o.tile_stride;
-    for (size_t i = (size_t)blockIdx.x * kLaneBlock + threadIdx.x; i < nz; i += (size_t)gridDim.x * kLaneBlock)
-      o.tsum[i] = 0u;
-    if (blockIdx.x == 0)
-      for (uint32_t i = threadIdx.x; i < 2u * S * o.n_chunks; i += kLaneBlock) reinterpret_cast<uint32_t*>(o.spine_lb)[i] = 0u;
-    return;
-  }
+  // every slot placed: nothing to do (k_spine zeroed their tile sums; their look-back words were
+  // never written)
+  if (S <= 64u && pmask == (~0ull >> (64u - S))) return;
   uint32_t buf = 0;
   // a resident grid strides over the groups of kDT tiles (a launch of one workgroup per group spent
   // most of its time dispatching workgroups that only zero their tile sums when every slot is placed)
@@ -3386,8 +3390,12 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                        scx.spec, b.n);
   mark(kStageDownGather);
   if (S > 0) {
-    // (at most 8 resident 256-thread workgroups per CU; larger batches stride)
-    const uint32_t resident = 8u * (uint32_t)cfg.num_cus;
+    // (at most 8 resident 256-thread workgroups per CU; larger batches stride). Every slot with a
+    // speculative target: usually all placed and nothing to do but the launch, one per CU (a failed
+    // placement strides over the tiles)
+    bool all_spec = scx.spec && cfg.spec_h && S <= 64;
+    for (size_t k = 0; all_spec && k < S; ++k) all_spec = cfg.spec_h[k] != 0u;
+    const uint32_t resident = (all_spec ? 1u : 8u) * (uint32_t)cfg.num_cus;
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus) {
       const uint32_t ng = (n_tiles + 3) / 4;
       hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3(ng < resident ? ng : resident), dim3(kLaneBlock), 0, st, b,
