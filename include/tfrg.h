@@ -124,7 +124,8 @@ int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
  * template's dict without a walk (its values are still read from the record; k_tpl_lane, schemas of
  * <= 16 slots, CRC verdicts on). Learned automatically from the first tfrg_decode_host
  * batch after each tfrg_set_schema; device-only callers pass a host sample here. Returns the number
- * of templates (0..4). tfrg_ctx_set_templates(ctx, 0) disables them (env TFRG_TEMPLATES=0). */
+ * of templates (0..4). tfrg_ctx_set_templates(ctx, 0) disables the match (env TFRG_TEMPLATES=0);
+ * the speculative placement of slots that are one inline value in every learned shape stays on. */
 int tfrg_learn_templates(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                          const uint64_t* h_end, uint32_t n, uint32_t flags);
 int tfrg_template_count(tfrg_ctx* ctx);

@@ -357,7 +357,10 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.tpl = c->tpl.as<uint32_t>();
   s.n_tpl = c->tpl_on ? c->n_tpl : 0u;
   s.tpl_w = c->tpl_w;
-  s.spec = c->tpl_on && c->spec_on && c->have_spec && c->n_tpl ? c->spec.as<uint32_t>() : nullptr;
+  // speculative placement is a property of the learned shapes' schema (a slot that is one inline
+  // value in every shape), not of the template match: it stays on with the templates off, where
+  // k_lane_count places those values itself
+  s.spec = c->spec_on && c->have_spec && c->n_tpl ? c->spec.as<uint32_t>() : nullptr;
   return s;
 }
 

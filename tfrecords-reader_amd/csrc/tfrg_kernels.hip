@@ -2838,6 +2838,20 @@ __device__ __forceinline__ bool hdr_0a_v(const FastSrc& s, uint32_t lo, uint32_t
   return (w & 0xffu) == 0x0au && (h < 4u || b3 < 0x80u) && bo + bl == lo + ll;
 }
 
+// max of two wave-uniform values on the scalar unit (max(a, b) - b is otherwise selected as a VALU
+// saturating subtract)
+__device__ __forceinline__ uint32_t smax_u32(uint32_t a, uint32_t b) {
+  uint32_t r;
+  asm("s_max_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
+  return r;
+}
+// lanes in the scalar lane mask `m` take b, the others keep a (one v_cndmask with an SGPR-pair mask)
+__device__ __forceinline__ uint32_t sel_mask(uint32_t a, uint32_t b, uint64_t m) {
+  uint32_t r;
+  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+  return r;
+}
+
 // Terminator bytes (< 0x80) among stage bytes [x0, x1) at stage offset `base`.
 __device__ __forceinline__ uint32_t count_terms(const uint8_t* l, uint32_t base, uint32_t x0, uint32_t x1) {
   uint32_t n = 0;
@@ -3017,7 +3031,9 @@ __device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bo
     const uint64_t pm = m & lt;
     const int pl = pm ? 63 - __builtin_clzll(pm) : (int)lane;
     const uint32_t pbe = (uint32_t)__shfl((int)be, pl, 64);
-    if (__ballot(iv && ((pm && pbe > bs) || ((dst + c) >> 32) != 0u))) return -1;
+    // (every value of the wave below 2^29 and inside the column: pass B's stores are the scalar
+    // column base + a 32-bit byte offset, no per-value capacity test)
+    if (__ballot(iv && ((pm && pbe > bs) || ((dst + c) >> 29) != 0u || dst + c > o.cap_i64))) return -1;
   }
   const uint32_t n = iv ? c : 0u;
   const uint32_t incl = wave_incl_scan_u32(n, lane);
@@ -3046,40 +3062,61 @@ __device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bo
     const bool ok = act && vi < scn && nb - 1u < 10u && (vi + 1u < scn || pe + 1u == sbe);
     bad |= act && !ok;
     const int64_t v = varint_term<COMPAT>(fs.l, ok ? s : 0u);
-    const uint64_t at = (uint64_t)pd + vi;
-    if (ok && at < o.cap_i64) o.i64[at] = v;
+    const uint32_t at = pd + vi;  // (< 2^29)
+    if (ok) *reinterpret_cast<int64_t*>(reinterpret_cast<uint8_t*>(o.i64) + (at << 3)) = v;
     gb += avail;
     rb += avail;
     if (rb >= kRingN) rb -= kRingN;
   };
   uint32_t wn = Q0 + 4u * lane < Qend ? L32[(Q0 >> 2) + lane] : 0u;  // (each step's dword read one step ahead)
+  uint64_t mrem = m;  // (scalar) eligible bodies not yet passed (bodies ascend with the slot index)
   for (uint32_t Qw = Q0; Qw < Qend; Qw += 256u) {
     const uint32_t Q = Qw + 4u * lane;
     const uint32_t w = wn;
     wn = Q + 256u < Qend ? L32[(Q + 256u) >> 2] : 0u;
-    uint32_t bm = 0, ks = 0;  // bytes of this dword inside an eligible body (bodies are >= 8 bytes apart)
-    uint64_t mw = __ballot(iv && bs < Qw + 256u && be > Qw);  // bodies overlapping this step
-    while (mw) {
+    // bytes of this lane's dword inside an eligible body (bodies are >= 8 bytes apart: at most one
+    // per dword) and its slot. Per body overlapping the step, its lanes [f, l] and the byte masks of
+    // its first and last lane are scalar; the lanes then take them in 5 selects
+    uint32_t bm = 0, ks = 0;
+    for (uint64_t mw = mrem; mw; mw &= mw - 1ull) {  // (scalar loop)
       const uint32_t k = (uint32_t)__builtin_ctzll(mw);
-      mw &= mw - 1ull;
       const uint32_t sbs = __builtin_amdgcn_readlane(bs, k), sbe = __builtin_amdgcn_readlane(be, k);
-      const uint32_t lo = sbs > Q ? sbs - Q : 0u, hi = sbe > Q ? sbe - Q : 0u;
-      if (hi > lo && lo < 4u) {
-        bm = bytes_mask(hi) & ~bytes_mask(lo);
-        ks = k;
+      if (sbe <= Qw) {  // ended before this step (always the lowest remaining one)
+        mrem &= mrem - 1ull;
+        continue;
       }
+      if (sbs >= Qw + 256u) break;
+      const uint32_t rs = smax_u32(sbs, Qw) - Qw, re = (sbe < Qw + 256u ? sbe : Qw + 256u) - Qw;  // step bytes [rs, re)
+      const uint32_t f = rs >> 2, l = (re - 1u) >> 2;
+      const uint64_t lm = (l == 63u ? ~0ull : (2ull << l) - 1ull) & ~((1ull << f) - 1ull);  // lanes f..l
+      const uint32_t ml = (re & 3u) ? (1u << (8u * (re & 3u))) - 1u : 0xffffffffu;
+      const uint32_t vf = (0xffffffffu << (8u * (rs & 3u))) & (f == l ? ml : 0xffffffffu);  // lane f's bytes
+      const uint64_t mlf = 1ull << f, mll = f == l ? 0ull : 1ull << l;
+      bm = sel_mask(bm, 0xffffffffu, lm);  // (lane masks in SGPRs: one select each)
+      bm = sel_mask(bm, vf, mlf);
+      bm = sel_mask(bm, ml, mll);
+      ks = sel_mask(ks, k, lm);
+      if (sbe > Qw + 256u) break;  // continues into the next step: the later bodies start there
     }
     uint32_t t = ~w & 0x80808080u & bm;
     const uint32_t nt = (uint32_t)__popc(t);
+    // this lane's first ring entry: terminators of the lanes below (three ballots of nt's bits)
     const uint64_t b0 = __ballot(nt & 1u), b1 = __ballot(nt & 2u), b2 = __ballot(nt & 4u);
-    uint32_t at = rh + (uint32_t)__popcll(b0 & lt) + 2u * (uint32_t)__popcll(b1 & lt) + 4u * (uint32_t)__popcll(b2 & lt);
+    const uint32_t c0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, rh));
+    const uint32_t c1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+    const uint32_t c2 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, 0u));
+    const uint32_t at = c0 + 2u * c1 + 4u * c2;
     const uint32_t tot = (uint32_t)__popcll(b0) + 2u * (uint32_t)__popcll(b1) + 4u * (uint32_t)__popcll(b2);
-    while (t) {
-      const uint32_t a = at >= kRingN ? at - kRingN : at;
-      ring[a] = (uint16_t)(Q + ((uint32_t)__builtin_ctz(t) >> 3));
-      ring_k[a] = (uint8_t)ks;
-      t &= t - 1u;
-      ++at;
+    // its (up to 4) entries, unrolled (a loop ran to the wave's largest count with loop control)
+#pragma unroll
+    for (uint32_t i = 0; i < 4u; ++i) {
+      if (!__ballot(i < nt)) break;  // (scalar)
+      if (i < nt) {
+        const uint32_t a0 = at + i, a = a0 >= kRingN ? a0 - kRingN : a0;
+        ring[a] = (uint16_t)(Q + ((uint32_t)__builtin_ctz(t) >> 3));
+        ring_k[a] = (uint8_t)ks;
+        t &= t - 1u;
+      }
     }
     gtot += tot;
     rh += tot;
@@ -3105,18 +3142,22 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
+  // (per list a scalar column pointer and store limit: the stores take the scalar base + the lane's
+  // 32-bit offset, the capacity check is one compare)
   constexpr int kFG = 8;
   uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
   while (m) {
-    uint32_t fb[kFG], fn[kFG];
-    uint64_t fd[kFG];
+    uint32_t fb[kFG], fn[kFG], lim[kFG];
+    uint32_t* fp[kFG];
     uint32_t nm = 0;
 #pragma unroll
     for (int i = 0; i < kFG; ++i) {
       const int k = m ? __builtin_ctzll(m) : 0;
       fn[i] = m ? __builtin_amdgcn_readlane(bl, k) >> 2 : 0u;
       fb[i] = fs.p + __builtin_amdgcn_readlane(bo, k);
-      fd[i] = readlane_u64(dst, k);
+      const uint64_t d = readlane_u64(dst, k);
+      lim[i] = d >= o.cap_f32 ? 0u : (o.cap_f32 - d < fn[i] ? (uint32_t)(o.cap_f32 - d) : fn[i]);
+      fp[i] = o.f32 + (d < o.cap_f32 ? d : 0ull);
       nm = nm > fn[i] ? nm : fn[i];
       m &= m - 1;
     }
@@ -3126,7 +3167,7 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
       for (int i = 0; i < kFG; ++i) x[i] = lds_u32u(fs.l, fb[i] + 4u * (j < fn[i] ? j : 0u));
 #pragma unroll
       for (int i = 0; i < kFG; ++i)
-        if (j < fn[i] && fd[i] + j < o.cap_f32) o.f32[fd[i] + j] = x[i];
+        if (j < lim[i]) fp[i][j] = x[i];
     }
   }
   PHASE_MARK(gf);
