@@ -82,6 +82,25 @@ def test_golden_cases_bit_exact(dec, orc, lane_max, wave_stage):
     assert not bad, "\n".join(bad[:15])
 
 
+def test_host_decode_equals_device_on_golden_cases(dec):
+    """The single-record host decode (tfrg_host_decode: the "cython" type, decode(raw), ds[i]) and
+    the device batch agree on every reference case: status, aux and entries (compat varints)."""
+    from tfr_reader import host
+
+    cases = G.load_cases()
+    payloads = [bytes.fromhex(c["payload"]) for c in cases]
+    r = dec.decode(*payload_batch(payloads), payload_only=True)
+    bad = []
+    for i, c in enumerate(cases):
+        st, aux, ent = host.decode_raw(payloads[i])
+        dst, daux = int(r.status[i]), int(r.aux[i])
+        if st != dst or (st and aux != daux):
+            bad.append((c["name"], st, dst, aux, daux))
+        elif st == 0 and G.canon_entries(ent) != G.canon_entries(raw_entries(r, i)):
+            bad.append((c["name"], "entries"))
+    assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("name", G.FILES)
 def test_golden_files_framed(dec, name):
     data, meta = G.load_file(name)

@@ -3197,10 +3197,18 @@ template <bool COMPAT>
 __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const DevOut& o, uint8_t* stage,
                                   uint16_t* ring, uint64_t placed) {
   const uint32_t lane = threadIdx.x & 63u, wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t nbig = o.info[kInfoBig];
-  if (blockIdx.x * kWavesPerBlock + wib >= nbig) return;  // wave-uniform: no records for this wave
-  const uint32_t stride = gridDim.x * kWavesPerBlock;
-  uint32_t i = blockIdx.x * kWavesPerBlock + wib;
+  // Each XCD takes one contiguous eighth of the list (workgroups b and b + 8 share an XCD): the
+  // slot metadata of neighbouring records shares 128-byte lines ([slot][n] columns), which its L2
+  // then fetches once instead of once per XCD
+  // (grids of fewer than 8 workgroups: one range)
+  const uint32_t nall = o.info[kInfoBig];
+  const uint32_t nx = gridDim.x >= 8u ? 8u : 1u;
+  const uint32_t xcd = blockIdx.x % nx, nbx = (gridDim.x - xcd + nx - 1u) / nx;
+  const uint32_t i0 = (uint32_t)((uint64_t)nall * xcd / nx), nbig = (uint32_t)((uint64_t)nall * (xcd + 1u) / nx);
+  const uint32_t w0 = i0 + (blockIdx.x / nx) * kWavesPerBlock + wib;
+  if (w0 >= nbig) return;  // wave-uniform: no records for this wave
+  const uint32_t stride = nbx * kWavesPerBlock;
+  uint32_t i = w0;
   RecPipe q;
   q.r1 = i < nbig ? o.big_list[i] : 0u;
   q.s1 = B.start[q.r1];
