@@ -2838,20 +2838,6 @@ __device__ __forceinline__ bool hdr_0a_v(const FastSrc& s, uint32_t lo, uint32_t
   return (w & 0xffu) == 0x0au && (h < 4u || b3 < 0x80u) && bo + bl == lo + ll;
 }
 
-// max of two wave-uniform values on the scalar unit (max(a, b) - b is otherwise selected as a VALU
-// saturating subtract)
-__device__ __forceinline__ uint32_t smax_u32(uint32_t a, uint32_t b) {
-  uint32_t r;
-  asm("s_max_u32 %0, %1, %2" : "=s"(r) : "s"(a), "s"(b));
-  return r;
-}
-// lanes in the scalar lane mask `m` take b, the others keep a (one v_cndmask with an SGPR-pair mask)
-__device__ __forceinline__ uint32_t sel_mask(uint32_t a, uint32_t b, uint64_t m) {
-  uint32_t r;
-  asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
-  return r;
-}
-
 // Terminator bytes (< 0x80) among stage bytes [x0, x1) at stage offset `base`.
 __device__ __forceinline__ uint32_t count_terms(const uint8_t* l, uint32_t base, uint32_t x0, uint32_t x1) {
   uint32_t n = 0;
@@ -3069,34 +3055,21 @@ __device__ __forceinline__ int int64_ring(const FastSrc& fs, const DevOut& o, bo
     if (rb >= kRingN) rb -= kRingN;
   };
   uint32_t wn = Q0 + 4u * lane < Qend ? L32[(Q0 >> 2) + lane] : 0u;  // (each step's dword read one step ahead)
-  uint64_t mrem = m;  // (scalar) eligible bodies not yet passed (bodies ascend with the slot index)
   for (uint32_t Qw = Q0; Qw < Qend; Qw += 256u) {
     const uint32_t Q = Qw + 4u * lane;
     const uint32_t w = wn;
     wn = Q + 256u < Qend ? L32[(Q + 256u) >> 2] : 0u;
-    // bytes of this lane's dword inside an eligible body (bodies are >= 8 bytes apart: at most one
-    // per dword) and its slot. Per body overlapping the step, its lanes [f, l] and the byte masks of
-    // its first and last lane are scalar; the lanes then take them in 5 selects
+    // bytes [lo, hi) of this lane's dword inside an eligible body (bodies are >= 8 bytes apart: at
+    // most one per dword) and its slot; the bodies overlapping the step from one ballot
     uint32_t bm = 0, ks = 0;
-    for (uint64_t mw = mrem; mw; mw &= mw - 1ull) {  // (scalar loop)
+    for (uint64_t mw = __ballot(iv && bs < Qw + 256u && be > Qw); mw; mw &= mw - 1ull) {
       const uint32_t k = (uint32_t)__builtin_ctzll(mw);
       const uint32_t sbs = __builtin_amdgcn_readlane(bs, k), sbe = __builtin_amdgcn_readlane(be, k);
-      if (sbe <= Qw) {  // ended before this step (always the lowest remaining one)
-        mrem &= mrem - 1ull;
-        continue;
+      const uint32_t lo = sbs > Q ? sbs - Q : 0u, hi0 = sbe > Q ? sbe - Q : 0u, hi = hi0 < 4u ? hi0 : 4u;
+      if (hi > lo) {  // (1 <= hi <= 4, lo <= 3: both shifts below 32)
+        bm = (0xffffffffu >> (32u - 8u * hi)) & (0xffffffffu << (8u * lo));
+        ks = k;
       }
-      if (sbs >= Qw + 256u) break;
-      const uint32_t rs = smax_u32(sbs, Qw) - Qw, re = (sbe < Qw + 256u ? sbe : Qw + 256u) - Qw;  // step bytes [rs, re)
-      const uint32_t f = rs >> 2, l = (re - 1u) >> 2;
-      const uint64_t lm = (l == 63u ? ~0ull : (2ull << l) - 1ull) & ~((1ull << f) - 1ull);  // lanes f..l
-      const uint32_t ml = (re & 3u) ? (1u << (8u * (re & 3u))) - 1u : 0xffffffffu;
-      const uint32_t vf = (0xffffffffu << (8u * (rs & 3u))) & (f == l ? ml : 0xffffffffu);  // lane f's bytes
-      const uint64_t mlf = 1ull << f, mll = f == l ? 0ull : 1ull << l;
-      bm = sel_mask(bm, 0xffffffffu, lm);  // (lane masks in SGPRs: one select each)
-      bm = sel_mask(bm, vf, mlf);
-      bm = sel_mask(bm, ml, mll);
-      ks = sel_mask(ks, k, lm);
-      if (sbe > Qw + 256u) break;  // continues into the next step: the later bodies start there
     }
     uint32_t t = ~w & 0x80808080u & bm;
     const uint32_t nt = (uint32_t)__popc(t);
