@@ -3115,32 +3115,45 @@ __device__ __forceinline__ void stage_gather_group(const FastSrc& fs, const DevO
   bool fail = present && kind != TFRG_KIND_BYTES && !packed;
   // canonical float lists: lane j moves value j (contiguous 4-byte stores), four lists per pass so
   // that four LDS reads are in flight before the stores
-  // (per list a scalar column pointer and store limit: the stores take the scalar base + the lane's
-  // 32-bit offset, the capacity check is one compare)
+  // Per list, computed by its own lane (slot) first: the stage offset of its values, the last one's
+  // offset, the values that fit the column and the column address; each list then takes one buffer
+  // resource bounded at its fitting values, so a store past them is dropped by the hardware (no
+  // per-value test, no exec-mask bookkeeping per list). The per-list work was scalar 64-bit
+  // arithmetic (~30 SALU per list) and cost C3 as much as the copies.
   constexpr int kFG = 8;
-  uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);
-  while (m) {
-    uint32_t fb[kFG], fn[kFG], lim[kFG];
-    uint32_t* fp[kFG];
-    uint32_t nm = 0;
+  const bool isf = packed && kind == TFRG_KIND_FLOAT;
+  uint64_t m = __ballot(isf);
+  if (m) {
+    // (lanes that are no float list hold zeros: a group past the last list re-reads lane 63, whose
+    // stores are then either dropped (no values) or the same values again)
+    const uint32_t fn_l = isf ? bl >> 2 : 0u, fb_l = fs.p + (isf ? bo : 0u), fo_l = fn_l ? 4u * (fn_l - 1u) : 0u;
+    const uint64_t d_l = dst < o.cap_f32 ? dst : o.cap_f32;
+    const uint32_t lim_l = o.cap_f32 - d_l < fn_l ? (uint32_t)(o.cap_f32 - d_l) : fn_l;
+    const uint64_t a_l = reinterpret_cast<uint64_t>(o.f32 + d_l);
+    const uint32_t j4 = 4u * lane;
+    while (m) {
+      uint32_t fb[kFG], fo[kFG];
+      __amdgpu_buffer_rsrc_t rs[kFG];
+      uint32_t nm = 0;
 #pragma unroll
-    for (int i = 0; i < kFG; ++i) {
-      const int k = m ? __builtin_ctzll(m) : 0;
-      fn[i] = m ? __builtin_amdgcn_readlane(bl, k) >> 2 : 0u;
-      fb[i] = fs.p + __builtin_amdgcn_readlane(bo, k);
-      const uint64_t d = readlane_u64(dst, k);
-      lim[i] = d >= o.cap_f32 ? 0u : (o.cap_f32 - d < fn[i] ? (uint32_t)(o.cap_f32 - d) : fn[i]);
-      fp[i] = o.f32 + (d < o.cap_f32 ? d : 0ull);
-      nm = nm > fn[i] ? nm : fn[i];
-      m &= m - 1;
-    }
-    for (uint32_t j = lane; j < nm; j += 64) {
-      uint32_t x[kFG];
+      for (int i = 0; i < kFG; ++i) {
+        const int k = __builtin_ctzll(m | (1ull << 63));
+        m &= m - 1ull;
+        const uint32_t fn = __builtin_amdgcn_readlane(fn_l, k), lim = __builtin_amdgcn_readlane(lim_l, k);
+        fb[i] = __builtin_amdgcn_readlane(fb_l, k);
+        fo[i] = __builtin_amdgcn_readlane(fo_l, k);
+        const uint64_t a = readlane_u64(a_l, k);  // (readlane returns int: a plain OR would sign-extend)
+        rs[i] = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(a), (short)0, (int)(4u * lim), 0x00020000);
+        nm = nm > fn ? nm : fn;
+      }
+      for (uint32_t j = 0; j < nm; j += 64) {  // (wave-uniform)
+        const uint32_t off = 4u * j + j4;
+        uint32_t x[kFG];
 #pragma unroll
-      for (int i = 0; i < kFG; ++i) x[i] = lds_u32u(fs.l, fb[i] + 4u * (j < fn[i] ? j : 0u));
+        for (int i = 0; i < kFG; ++i) x[i] = lds_u32u(fs.l, fb[i] + (off < fo[i] ? off : fo[i]));
 #pragma unroll
-      for (int i = 0; i < kFG; ++i)
-        if (j < lim[i]) fp[i][j] = x[i];
+        for (int i = 0; i < kFG; ++i) __builtin_amdgcn_raw_buffer_store_b32(x[i], rs[i], off, 0, 0);
+      }
     }
   }
   PHASE_MARK(gf);

@@ -34,6 +34,12 @@ VARIANTS = {
     # k_tpl_lane at 8 waves/SIMD (64 VGPRs: 4 workgroups per CU instead of 3; spills a few registers)
     "lb8": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
              "__launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2))")],
+    # k_tail_gather without the float copies / the packed int64 decode / int64_ring's pass B
+    # (VALU attribution by PMC; wrong results)
+    "g_nofloat": [("tfrg_kernels.hip", "  uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);", "  uint64_t m = 0;")],
+    "g_noint64": [("tfrg_kernels.hip", "  int rr = int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring);", "  int rr = 1;")],
+    "g_nopassb": [("tfrg_kernels.hip", "    while (gtot - gb >= 64u) pass_b(64u);\n", "    gb = gtot;\n"),
+                  ("tfrg_kernels.hip", "  if (gtot > gb) pass_b(gtot - gb);", "  gb = gtot;")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
