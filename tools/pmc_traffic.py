@@ -47,7 +47,8 @@ def main() -> None:
     line = json.loads((out / "FETCH_SIZE.log").read_text().strip().splitlines()[-1])
     records, launches = line["config"]["records_per_gpu"], line["config"]["batches_per_gpu"]
     res = {"config": workload, "records": records, "launches_per_step": launches,
-           "kernel": name.split("(")[0], "fetch_size_kb": fetch_kb, "write_size_kb": write_kb,
+           "kernel": name.replace("(anonymous namespace)::", "").split("(")[0], "fetch_size_kb": fetch_kb,
+           "write_size_kb": write_kb,
            "traffic_bytes": fetch_kb * 1024 * 2 + write_kb * 1024,
            "correction": "FETCH_SIZE x2 (gfx950 128-B fills tallied at 64 B), WRITE_SIZE as read"}
     (out / f"traffic_{workload}.json").write_text(json.dumps(res, indent=1))
