@@ -1952,6 +1952,8 @@ __device__ __forceinline__ uint32_t rl32(uint32_t x, uint32_t k) {
 struct CrcWin {
   uint64_t base;  // first flat round (entry k's rounds: [base[k], base[k + 1]))
   uint64_t a, b;  // payload [a, b)
+  uint32_t e32;   // E of entry k (crc_ent) mod 2^32: the byte offset of its chunk for flat round R and
+                  // lane l is (e32 + 64 R - l) << 4 (batches are < 4 GiB)
 };
 
 __device__ __forceinline__ CrcWin crc_win_load(const DevBatch& B, const DevOut& o, uint32_t win0, uint32_t nrec,
@@ -1963,6 +1965,10 @@ __device__ __forceinline__ CrcWin crc_win_load(const DevBatch& B, const DevOut& 
     const RecView v = rec_view(B, o.crc_rec[idx]);
     w.a = v.p0;
     w.b = v.e - 4;
+  }
+  {  // E = c1 - 64 (J - 1) - 64 base[k] = c1 - 64 base[k + 1] + 64
+    const uint32_t nb = (uint32_t)__shfl_down((int)(uint32_t)w.base, 1, 64);
+    w.e32 = (uint32_t)((w.b - 1u) >> 4) - 64u * nb + 64u;
   }
   // the window's loads retired here: the group loads issued after it then carry no false wait on
   // them (a merged loop-header state otherwise drains vmcnt before every group)
@@ -2075,6 +2081,9 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   __syncthreads();
   const RotTabView T{reinterpret_cast<const uint8_t*>(lds)};
   const bool tab_at0 = (uint32_t)(uintptr_t)lds == 0u;  // (the asm chunk path addresses LDS 0)
+  // the batch's readable bytes (round_up(nbytes, 16) < 2^32) as a buffer resource
+  const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)((B.nbytes + 15u) & ~15ull), 0x00020000);
   const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
   const CrcRot RR = crc_rot_init(lane);
   const uint64_t W = (uint64_t)gridDim.x * (BLK / 64), wv = (uint64_t)blockIdx.x * (BLK / 64) + wib;
@@ -2115,16 +2124,17 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     const uint64_t rl = Rs + g.n - 1u;
     const uint32_t k0 = (uint32_t)__popcll(__ballot(w.base <= Rs)) - 1u;
     const uint32_t kl = (uint32_t)__popcll(__ballot(w.base <= rl)) - 1u;
+    // Chunk loads through a buffer resource over the batch with 32-bit offsets: a chunk before the
+    // batch (a negative offset, i.e. a huge one) reads zeros, a chunk of the previous record is
+    // read as it is; both occur only in a record's edge rounds, whose masked path (process) never
+    // uses those lanes' bytes. Loads past the group's rounds re-read later bytes and are unused.
     if (k0 == kl) {  // (scalar) the whole group inside one record: its entry once
-      const CrcEnt e = crc_ent(w, k0);
-      const uint64_t ch0 = e.E + 64ull * Rs - lane;
+      const uint32_t vo = (rl32(w.e32, k0) + 64u * (uint32_t)Rs - lane) << 4;
 #pragma unroll
       for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
-        const uint32_t dd = (uint32_t)d < g.n ? (uint32_t)d : g.n - 1u;
-        g.rd[d] = Rs + dd;
+        g.rd[d] = Rs + ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u);
         g.kd[d] = k0;
-        const uint64_t ch = ch0 + 64ull * dd;
-        g.wd[d] = *reinterpret_cast<const uint4*>(B.bytes + (((int64_t)ch >= (int64_t)e.c0 ? ch : e.c0) << 4));
+        g.wd[d] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo + 1024u * d, 0, 0));
       }
       return;
     }
@@ -2132,10 +2142,8 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     for (int d = 0; d < kCrcDepth; ++d) {  // every load of the group in flight before any use
       g.rd[d] = Rs + ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u);
       g.kd[d] = (uint32_t)__popcll(__ballot(w.base <= g.rd[d])) - 1u;
-      const CrcEnt e = crc_ent(w, g.kd[d]);
-      const uint64_t c0 = e.c0;
-      const uint64_t ch = e.E + 64ull * g.rd[d] - lane;
-      g.wd[d] = *reinterpret_cast<const uint4*>(B.bytes + (((int64_t)ch >= (int64_t)c0 ? ch : c0) << 4));
+      const uint32_t vo = (rl32(w.e32, g.kd[d]) + 64u * (uint32_t)g.rd[d] - lane) << 4;
+      g.wd[d] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo, 0, 0));
     }
   };
   auto process = [&](const Grp& g) {
