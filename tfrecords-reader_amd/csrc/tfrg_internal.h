@@ -74,6 +74,7 @@ struct LeanArgs {
   uint32_t* tsum;  // tile sums, slot k's at k * tile_stride
   uint32_t n_slots;
   uint32_t tile_stride;
+  uint32_t half;   // (launch_tpl_lane) a wave takes half a tile: small batches, twice the waves
   LeanTgt tg[kLeanMaxSlots];
 };
 

@@ -99,8 +99,11 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   static_assert(kTileShift == 8, "4 groups of 64 records per tile");
   const uint32_t ntiles = (ngroups + 3u) >> 2;
   const uint32_t nw = gridDim.x * kWaves;
-  const uint32_t t0 = blockIdx.x * kWaves + wib;
-  if (t0 >= ntiles) return;  // (wave-uniform; no barrier follows)
+  // (A.half: wave w takes the groups 2w, 2w + 1, one step, and adds its tile sums atomically: a
+  // batch too small to give every CU a workgroup runs on twice the waves)
+  const uint32_t w0 = blockIdx.x * kWaves + wib;
+  const uint32_t t0 = A.half ? w0 >> 1 : w0;
+  if (t0 >= ntiles || (A.half && 4u * t0 + ((w0 & 1u) << 1) >= ngroups)) return;  // (wave-uniform; no barrier follows)
   // Two groups per step (g, g + 1 of the wave's tile), their windows loaded together: a step waits
   // once, for both windows and the previous step's column stores (gfx9 counts stores in vmcnt, in
   // issue order), so each wait covers 128 records. The offsets of the next step are requested
@@ -248,10 +251,10 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
   };
   // the wave's steps: tile t0 + k nw, groups (4t, 4t+1), (4t+2, 4t+3)
-  uint32_t t = t0, p = 0;
+  uint32_t t = t0, p = A.half ? (w0 & 1u) << 1 : 0u;
   uint64_t s0, e0, s1, e1;
-  offsets(4u * t, s0, e0);
-  offsets(4u * t + 1u, s1, e1);
+  offsets(4u * t + p, s0, e0);
+  offsets(4u * t + p + 1u, s1, e1);
   while (t < ntiles) {
     const uint32_t ga = 4u * t + p, gb = ga + 1u;
     uint32_t wa[W], wb[W];
@@ -266,6 +269,10 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     if (gb < ngroups) proc(wb, gb, sb, eb);
     // the tile's sums: the first writer of tsum (zero before the decode; k_lane_count's residual
     // records add theirs with atomics after this kernel)
+    if (A.half) {  // (wave-uniform) the other half of the tile is another wave's
+      if (lane < A.n_slots && acc) atomicAdd(&A.tsum[lane * A.tile_stride + t], acc);
+      break;
+    }
     if (p || gb + 1u >= ngroups) {
       if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + t] = acc;
       acc = 0;
@@ -288,12 +295,14 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   // the waves that drew an extra round of tiles (c4of8: 0.414 ms against 0.430 ms for one round of
   // resident workgroups; the 32 KiB table copy per workgroup is L2 traffic)
   const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;
-  const dim3 grid(need ? (need + per_wave - 1u) / per_wave : 1u);
+  LeanArgs a2 = a;
+  a2.half = need < (uint32_t)num_cus ? 1u : 0u;  // (fewer workgroups than CUs: half a tile per wave)
+  const dim3 grid(a2.half ? (tiles * 2u + kTplBlock / 64 - 1) / (kTplBlock / 64) : need ? (need + per_wave - 1u) / per_wave : 1u);
   const uint32_t* tabs = d_tab + kLeanTabOff;
   switch (w) {
-    case 16: hipLaunchKernelGGL(k_tpl_lane<16>, grid, dim3(kTplBlock), 0, st, b, o, a, tpl, tabs); break;
-    case 32: hipLaunchKernelGGL(k_tpl_lane<32>, grid, dim3(kTplBlock), 0, st, b, o, a, tpl, tabs); break;
-    case 64: hipLaunchKernelGGL(k_tpl_lane<64>, grid, dim3(kTplBlock), 0, st, b, o, a, tpl, tabs); break;
+    case 16: hipLaunchKernelGGL(k_tpl_lane<16>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
+    case 32: hipLaunchKernelGGL(k_tpl_lane<32>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
+    case 64: hipLaunchKernelGGL(k_tpl_lane<64>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -1,8 +1,7 @@
 set -u
 O=gpurun_out/r4l; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests/test_crc_stream_gpu.py tests/test_gpu_parity.py tests/test_large_records_gpu.py tests/test_c2_full_gpu.py > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests/test_templates_gpu.py tests/test_spec_gpu.py tests/test_gpu_parity.py tests/test_c4_gpu.py > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
 tail -2 $O/t.log
-STEPS=50 bash tools/ab.sh c2 libtfrg.so || exit 1
-STEPS=20 bash tools/ab.sh c4c2 libtfrg.so || exit 1
-STEPS=20 bash tools/ab.sh c3 libtfrg.so || exit 1
+STEPS=100 bash tools/ab.sh c1file libtfrg.so || exit 1
+STEPS=50 bash tools/ab.sh c4of8 libtfrg.so || exit 1

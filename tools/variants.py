@@ -31,6 +31,11 @@ VARIANTS = {
                       "    const uint32_t voff = full ? ((gg * 3712u) & ~15u) + 16u * lane - 48u * lane / 16u * 0u : 0xffffff00u;"),
                      ("tfrg_tpl.hip", "raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0)",
                       "raw_buffer_load_b128(rsrc, voff + 1024u * q, 0, 0)")],
+    # k_tpl_lane with four / three tiles per wave on large batches (fewer workgroups, table copies)
+    "tpw4": [("tfrg_tpl.hip", "const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;",
+              "const uint32_t per_wave = need >= 16u * (uint32_t)num_cus ? 4u : need >= 8u * (uint32_t)num_cus ? 2u : 1u;")],
+    "tpw3": [("tfrg_tpl.hip", "const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;",
+              "const uint32_t per_wave = need >= 12u * (uint32_t)num_cus ? 3u : need >= 8u * (uint32_t)num_cus ? 2u : 1u;")],
     # k_tpl_lane at 8 waves/SIMD (64 VGPRs: 4 workgroups per CU instead of 3; spills a few registers)
     "lb8": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
              "__launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2))")],
