@@ -1,7 +1,6 @@
 set -u
 O=gpurun_out/r4l; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests/test_templates_gpu.py tests/test_spec_gpu.py tests/test_gpu_parity.py tests/test_c4_gpu.py > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
-tail -2 $O/t.log
-STEPS=100 bash tools/ab.sh c1file libtfrg.so || exit 1
-STEPS=50 bash tools/ab.sh c4of8 libtfrg.so || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace2 -o run -- python bench.py --only c4of8 --no-cpu --steps 10 > $O/trace2.log 2>&1 || { tail $O/trace2.log; exit 1; }
+CSV=$(find $O/trace2 -name "*kernel_trace.csv" | head -1)
+python tools/trace_gaps.py $CSV k_tpl_lane 3

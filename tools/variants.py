@@ -31,6 +31,8 @@ VARIANTS = {
                       "    const uint32_t voff = full ? ((gg * 3712u) & ~15u) + 16u * lane - 48u * lane / 16u * 0u : 0xffffff00u;"),
                      ("tfrg_tpl.hip", "raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0)",
                       "raw_buffer_load_b128(rsrc, voff + 1024u * q, 0, 0)")],
+    # k_tail_count without role 1 (the exact walker): the streaming CRC's registers alone (timing only)
+    "crc_only": [("tfrg_kernels.hip", "  role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);\n", "")],
     # k_tpl_lane with four / three tiles per wave on large batches (fewer workgroups, table copies)
     "tpw4": [("tfrg_tpl.hip", "const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;",
               "const uint32_t per_wave = need >= 16u * (uint32_t)num_cus ? 4u : need >= 8u * (uint32_t)num_cus ? 2u : 1u;")],
