@@ -9,7 +9,7 @@ file, native copy into pinned staging (worker threads), native framing index, H2
 byte column), D2H of every column into numpy arrays. Two slots overlap staging/H2D of batch k+1
 with the decode of batch k. The page cache is warm (the files were just written; dropping it needs
 root): the rate is host memory -> values, not disk -> values. A second figure times turning a
-sample of records into Python ``Feature`` objects with every ``.value`` read (the reference's
+batch of records into Python ``Feature`` objects with every ``.value`` read (the reference's
 output form).
 
 usage: e2e.py [--config c1|c2|c3] [--files N] [--batch-mib M] [--out PATH]
@@ -48,7 +48,9 @@ def main():
     ap.add_argument("--config", default="c1", choices=["c1", "c2", "c3"])
     ap.add_argument("--files", type=int, default=None)
     ap.add_argument("--batch-mib", type=int, default=256)
-    ap.add_argument("--sample", type=int, default=100000, help="records turned into Python Feature values")
+    ap.add_argument("--sample", type=int, default=0,
+                    help="records of the last batch turned into Python Feature values (0: all of them: a "
+                         "batch's columns become Python objects once, so a part of a batch pays for all of it)")
     ap.add_argument("--out", default=None)
     ap.add_argument("--copy", action="store_true", help="copy each batch's columns out of the pinned buffers")
     a = ap.parse_args()
@@ -78,7 +80,7 @@ def main():
         timing = {k: round(v, 4) for k, v in sd.timing.items()}
         # Python Feature objects with every value read, on a sample of the last batch (its columns
         # may be views of the stream's pinned buffers: before the stream is closed)
-        k = min(a.sample, len(last))
+        k = len(last) if a.sample <= 0 else min(a.sample, len(last))
         t1 = time.perf_counter()
         feats = last.features(0, k)
         nv = 0

@@ -1,6 +1,7 @@
 set -u
-O=gpurun_out/r4l; mkdir -p $O
+O=gpurun_out/r4f; mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/trace2 -o run -- python bench.py --only c4of8 --no-cpu --steps 10 > $O/trace2.log 2>&1 || { tail $O/trace2.log; exit 1; }
-CSV=$(find $O/trace2 -name "*kernel_trace.csv" | head -1)
-python tools/trace_gaps.py $CSV k_tpl_lane 3
+for c in c1 c2 c3; do
+  timeout -k 10 300 python tools/e2e.py --config $c --out $O/e2e_$c.json > $O/e2e_$c.log 2>&1 || { tail $O/e2e_$c.log; exit 1; }
+  python3 -c "import json; d=json.load(open('$O/e2e_$c.json')); print('$c', d['GiB_s'], d['python_features'])"
+done
