@@ -1282,13 +1282,19 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
   return x;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t lane) {
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(v, d, 64);
-    if (lane >= (uint32_t)d) v += y;
-  }
-  return v;
+// Inclusive prefix sum over the wave (every lane active) in seven DPP adds, no LDS: rows of 16 by
+// row_shr 1, 2, 3 of the value, then 4 and 8 of the partial sums (bank masks: only the lanes that
+// still miss a part), then the row totals by row_bcast 15 / 31 (gfx9 DPP; lanes a mask leaves out
+// read `old` = 0). Replaces six ds_bpermute round trips of __shfl_up.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t) {
+  uint32_t s = v + (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);  // row_shr:1
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);             // row_shr:2
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);             // row_shr:3
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xf, 0xe, true);             // row_shr:4
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xf, 0xc, true);             // row_shr:8
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xa, 0xf, false);            // row_bcast:15
+  s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xc, 0xf, false);            // row_bcast:31
+  return s;
 }
 
 // 1 KiB rounds (64 lanes x aligned 16-byte chunks) covering the payload [a, b), b > a

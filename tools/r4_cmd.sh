@@ -1,7 +1,9 @@
 set -u
-O=gpurun_out/r4f; mkdir -p $O
+O=gpurun_out/r4l; mkdir -p $O
 export TMPDIR=/tmp
-for c in c1 c2 c3; do
-  timeout -k 10 300 python tools/e2e.py --config $c --out $O/e2e_$c.json > $O/e2e_$c.log 2>&1 || { tail $O/e2e_$c.log; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/e2e_$c.json')); print('$c', d['GiB_s'], d['python_features'])"
-done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests > $O/t.log 2>&1 || { tail -30 $O/t.log; exit 1; }
+tail -2 $O/t.log
+STEPS=30 bash tools/ab.sh c3 libtfrg.so || exit 1
+STEPS=50 bash tools/ab.sh c4of8 libtfrg.so || exit 1
+STEPS=50 bash tools/ab.sh c2 libtfrg.so || exit 1
+STEPS=100 bash tools/ab.sh c1file libtfrg.so || exit 1
