@@ -1276,12 +1276,6 @@ __device__ __forceinline__ void frame_verdicts(const DevBatch& B, RecView& v, co
   }
 }
 
-__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) x += __shfl_xor(x, m, 64);
-  return x;
-}
-
 // Inclusive prefix sum over the wave (every lane active) in seven DPP adds, no LDS: rows of 16 by
 // row_shr 1, 2, 3 of the value, then 4 and 8 of the partial sums (bank masks: only the lanes that
 // still miss a part), then the row totals by row_bcast 15 / 31 (gfx9 DPP; lanes a mask leaves out
@@ -1295,6 +1289,23 @@ __device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v, uint32_t) {
   s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xa, 0xf, false);            // row_bcast:15
   s += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xc, 0xf, false);            // row_bcast:31
   return s;
+}
+
+// wave total (every lane active), wave-uniform: the scan's last lane
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(x, 0u), 63);
+}
+
+// XOR of every lane's value (every lane active), wave-uniform: the scan above with XOR
+__device__ __forceinline__ uint32_t wave_xor_u32(uint32_t v) {
+  uint32_t s = v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x113, 0xf, 0xf, true);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x114, 0xf, 0xe, true);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x118, 0xf, 0xc, true);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x142, 0xa, 0xf, false);
+  s ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)s, 0x143, 0xc, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_readlane((int)s, 63);
 }
 
 // 1 KiB rounds (64 lanes x aligned 16-byte chunks) covering the payload [a, b), b > a
@@ -2006,9 +2017,7 @@ __device__ __forceinline__ void crc_flush(const uint8_t* lbase, const uint32_t* 
   const uint64_t bas = rl64(w.base, k);
   const uint32_t J = (uint32_t)(rl64(w.base, k + 1u) - bas);
   const uint32_t jtop = J - 1u - (uint32_t)(Rf - bas), jlo = J - 1u - (uint32_t)(Rl - bas);
-  uint32_t t = gf_mul(S, cst[lane]);
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t ^= (uint32_t)__shfl_xor((int)t, m, 64);
+  uint32_t t = wave_xor_u32(gf_mul(S, cst[lane]));
   if (jlo) {  // x x^(8192 jlo): one table multiply per set bit of jlo (wave-uniform: scalar loads)
     uint32_t u = rfl32(t);
     for (uint32_t kb = 0, jj = jlo; jj; ++kb, jj >>= 1) {
