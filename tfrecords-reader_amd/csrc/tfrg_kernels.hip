@@ -2096,9 +2096,12 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   __syncthreads();
   const RotTabView T{reinterpret_cast<const uint8_t*>(lds)};
   const bool tab_at0 = (uint32_t)(uintptr_t)lds == 0u;  // (the asm chunk path addresses LDS 0)
-  // the batch's readable bytes (round_up(nbytes, 16) < 2^32) as a buffer resource
+  // the batch's readable bytes (round_up(nbytes, 16), at most 2^32 - 1: batches are < 4 GiB) as a
+  // buffer resource
+  const uint64_t readable = (B.nbytes + 15u) & ~15ull;
   const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)((B.nbytes + 15u) & ~15ull), 0x00020000);
+      const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)(readable < 0xffffffffull ? readable : 0xffffffffull),
+      0x00020000);
   const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
   const CrcRot RR = crc_rot_init(lane);
   const uint64_t W = (uint64_t)gridDim.x * (BLK / 64), wv = (uint64_t)blockIdx.x * (BLK / 64) + wib;

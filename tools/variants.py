@@ -38,6 +38,8 @@ VARIANTS = {
               "const uint32_t per_wave = need >= 16u * (uint32_t)num_cus ? 4u : need >= 8u * (uint32_t)num_cus ? 2u : 1u;")],
     "tpw3": [("tfrg_tpl.hip", "const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;",
               "const uint32_t per_wave = need >= 12u * (uint32_t)num_cus ? 3u : need >= 8u * (uint32_t)num_cus ? 2u : 1u;")],
+    # k_tpl_lane with a whole tile (four groups) per step (no half-tile mode: large batches only)
+    "g4": [("tfrg_tpl.hip", "  uint32_t t = t0, p = A.half ? (w0 & 1u) << 1 : 0u;\n  uint64_t s0, e0, s1, e1;\n  offsets(4u * t + p, s0, e0);\n  offsets(4u * t + p + 1u, s1, e1);\n  while (t < ntiles) {\n    const uint32_t ga = 4u * t + p, gb = ga + 1u;\n    uint32_t wa[W], wb[W];\n    window(wa, in_batch(ga, s0, e0), e0, ga);\n    window(wb, in_batch(gb, s1, e1), e1, gb);\n    const uint64_t sa = s0, ea = e0, sb = s1, eb = e1;\n    // the next step's offsets\n    const uint32_t tn = p ? t + nw : t, pn = p ^ 2u;\n    offsets(4u * tn + pn, s0, e0);\n    offsets(4u * tn + pn + 1u, s1, e1);\n    proc(wa, ga, sa, ea);\n    if (gb < ngroups) proc(wb, gb, sb, eb);", '  uint32_t t = t0, p = 0u;\n  uint64_t s0, e0, s1, e1, s2, e2, s3, e3;\n  offsets(4u * t, s0, e0);\n  offsets(4u * t + 1u, s1, e1);\n  offsets(4u * t + 2u, s2, e2);\n  offsets(4u * t + 3u, s3, e3);\n  while (t < ntiles) {\n    const uint32_t ga = 4u * t, gb = ga + 1u;\n    uint32_t wa[W], wb[W], wc[W], wd[W];\n    window(wa, in_batch(ga, s0, e0), e0, ga);\n    window(wb, in_batch(gb, s1, e1), e1, gb);\n    window(wc, in_batch(ga + 2u, s2, e2), e2, ga + 2u);\n    window(wd, in_batch(ga + 3u, s3, e3), e3, ga + 3u);\n    const uint64_t sa = s0, ea = e0, sb = s1, eb = e1, sc = s2, ec = e2, sd = s3, ed = e3;\n    const uint32_t tn = t + nw, pn = 2u;\n    offsets(4u * tn, s0, e0);\n    offsets(4u * tn + 1u, s1, e1);\n    offsets(4u * tn + 2u, s2, e2);\n    offsets(4u * tn + 3u, s3, e3);\n    proc(wa, ga, sa, ea);\n    if (gb < ngroups) proc(wb, gb, sb, eb);\n    if (ga + 2u < ngroups) proc(wc, ga + 2u, sc, ec);\n    if (ga + 3u < ngroups) proc(wd, ga + 3u, sd, ed);\n    p = 2u;\n    const uint32_t gbb = ga + 3u;\n    if (gbb + 1u >= ngroups) { if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + t] = acc; break; }\n    if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + t] = acc;\n    acc = 0;\n    t = tn;\n    continue;')],
     # k_tpl_lane at 8 waves/SIMD (64 VGPRs: 4 workgroups per CU instead of 3; spills a few registers)
     "lb8": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
              "__launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2))")],
