@@ -318,10 +318,16 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     vals = 8 * kt[3] + 4 * kt[2] + 8 * kt[1]
     present_small = int(present * n_small / max(n, 1))
     n_tiles = sum((int(r1 - r0) + 255) // 256 for r0, r1, _, _ in plan.tolist())
-    lane_alg = small_bytes + n_small * (16 + 5 + 6 * n_slots) + 8 * present_small
+    # slots whose speculative placement is final in every batch: one value per record at row r, row
+    # splits implicit (tfrg_info.placed_slots, never stored): order only
+    placed = ~0
+    for i in infos:
+        placed &= int(i.placed_slots)
+    n_placed = bin(placed & ((1 << min(n_slots, 64)) - 1)).count("1")
+    lane_alg = small_bytes + n_small * (16 + 5 + 2 * n_slots + 4 * (n_slots - n_placed)) + 8 * present_small
     alg = {
-        # template path: its records' framed bytes + offsets in; status, verdict, order + row split
-        # (or count) per slot and a value / location word per present list out
+        # template path: its records' framed bytes + offsets in; status, verdict, order per slot, a row
+        # split (or count) per slot not placed, and a value / location word per present list out
         "k_tpl_lane": lane_alg,
         # lane kernel (all lane records when no template applies): the same compulsory bytes
         "k_lane_count": lane_alg,
@@ -338,7 +344,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
     n_keys = len(sd.keys.keys)
     R = framed + 16 * n
-    W = 4 * n + 4 * n * n_keys + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
+    # (SURVEY D2's W, less the row splits of placed slots, which are implicit: never stored)
+    W = 4 * n + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
     ms_step = elapsed / steps * 1e3
     out = {
         "workload": w.desc,
@@ -367,6 +374,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         },
         "pipeline": {
             "alg_bytes_R_plus_W": R + W,
+            "implicit_row_split_bytes": 4 * n * n_placed,
             "achieved_GBps": round((R + W) / (ms_step / 1e3) / 1e9, 1),
             "frac": round((R + W) / (ms_step / 1e3) / 1e9 / PEAK_HBM_GBS, 4),
         },

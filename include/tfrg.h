@@ -209,6 +209,10 @@ typedef struct tfrg_info {
   uint64_t bytes_data_len;  /* TFRG_FLAG_MATERIALIZE_BYTES: bytes in the byte column, else 0   */
   uint32_t tpl_groups_missed; /* 64-record groups with a record no record-shape template took */
   uint32_t reserved;
+  /* bit k: slot k (< 64) holds exactly one value per record, at row r of its column (final
+   * speculative placement). Its row splits are the identity 0..n and are NOT stored on the device
+   * (tfrg_result_device); tfrg_result_fetch writes them into the caller's buffer. */
+  uint64_t placed_slots;
 } tfrg_info;
 
 /* Waits for the last decode and returns its summary. */
@@ -216,6 +220,7 @@ int tfrg_result_info(tfrg_ctx* ctx, tfrg_info* info);
 
 /* Columnar result. Per record: status/aux/verdict. Per slot s (row-major [n_slots][n]):
  * order (0 absent, else 1 + the key's position in the record's dict), row_splits [n_slots][n+1]
+ * (device view: rows of tfrg_info.placed_slots are not stored, they are 0..n)
  * (element offsets inside the slot's column), slot_base [n_slots] (column start inside its kind's
  * value array). Values: int64, float bits, bytes views (absolute offset into the input buffer,
  * length). miss: [min(n_miss_entries, cap)][4] = (record, kind, key offset, key length). */

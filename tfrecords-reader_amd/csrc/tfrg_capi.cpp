@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <map>
+#include <numeric>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -963,6 +964,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->nbytes = c->nbytes;
   info->bytes_data_len = blen;
   info->tpl_groups_missed = h[kInfoResid];
+  info->placed_slots = ((uint64_t)h[kInfoPlacedHi] << 32) | h[kInfoPlacedLo];
   if (h[kInfoOverflow]) {
     set_error("value columns overflowed their capacity (overlapping ranges in a device batch): decode "
               "the ranges from host memory (tfrg_decode_host) or split the batch");
@@ -1003,7 +1005,17 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
   HIP_TRY(cp(h->aux, c->aux.p, n * 8));
   HIP_TRY(cp(h->verdict, c->verdict.p, n));
   HIP_TRY(cp(h->order, c->order.p, S * n * 2));
-  HIP_TRY(cp(h->row_splits, c->rs.p, S * (n + 1) * 4));
+  // row splits: a placed slot's are the identity (never stored on the device), written here while
+  // the other rows copy
+  if (h->row_splits) {
+    for (size_t k = 0; k < S; ++k) {
+      uint32_t* row = h->row_splits + k * (n + 1);
+      if (k < 64 && ((info.placed_slots >> k) & 1ull)) continue;
+      HIP_TRY(cp(row, c->rs.as<uint32_t>() + k * (n + 1), (n + 1) * 4));
+    }
+    for (size_t k = 0; k < S && k < 64; ++k)
+      if ((info.placed_slots >> k) & 1ull) std::iota(h->row_splits + k * (n + 1), h->row_splits + (k + 1) * (n + 1), 0u);
+  }
   HIP_TRY(cp(h->slot_base, c->slot_base.p, S * 8));
   // (clamped to the capacities: a result that overflowed them fails in tfrg_result_info above)
   auto cl = [](uint64_t v, uint64_t cap) { return v < cap ? v : cap; };

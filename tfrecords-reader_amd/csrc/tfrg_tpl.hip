@@ -218,8 +218,8 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
         }
         if (ok) {
           T.ord[r] = (uint16_t)rank;
-          if (T.kind) {  // speculative placement: value at column row r, row split r
-            T.rs[r] = r;
+          if (T.kind) {  // speculative placement: value at column row r; the row split r is implicit
+                         // (tfrg_info.placed_slots: a final placement's row splits are never stored)
             if (r < T.lim) {
               if (T.kind == TFRG_KIND_INT64) {
                 reinterpret_cast<uint64_t*>(T.v1)[r] = lx;

@@ -41,6 +41,7 @@ class TfrgInfo(C.Structure):
         ("bytes_data_len", C.c_uint64),
         ("tpl_groups_missed", C.c_uint32),
         ("reserved", C.c_uint32),
+        ("placed_slots", C.c_uint64),
     ]
 
 

@@ -49,6 +49,19 @@ VARIANTS = {
     "g_noint64": [("tfrg_kernels.hip", "  int rr = int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring);", "  int rr = 1;")],
     "g_nopassb": [("tfrg_kernels.hip", "    while (gtot - gb >= 64u) pass_b(64u);\n", "    gb = gtot;\n"),
                   ("tfrg_kernels.hip", "  if (gtot > gb) pass_b(gtot - gb);", "  gb = gtot;")],
+    # k_tpl_lane without the row-split stores of placed slots (identity rows; wrong row splits)
+    "nors": [("tfrg_tpl.hip", "            T.rs[r] = r;\n", "")],
+    # the same without the key-order stores too (wrong row splits and key order)
+    "nors_noord": [("tfrg_tpl.hip", "            T.rs[r] = r;\n", ""),
+                   ("tfrg_tpl.hip", "          T.ord[r] = (uint16_t)rank;\n", "")],
+    # int64_ring pass A: a body's byte mask in a dword from saturating subtractions
+    "c3bm": [("tfrg_kernels.hip",
+              "      const uint32_t lo = sbs > Q ? sbs - Q : 0u, hi0 = sbe > Q ? sbe - Q : 0u, hi = hi0 < 4u ? hi0 : 4u;\n"
+              "      if (hi > lo) {  // (1 <= hi <= 4, lo <= 3: both shifts below 32)\n"
+              "        bm = (0xffffffffu >> (32u - 8u * hi)) & (0xffffffffu << (8u * lo));\n",
+              "      const uint32_t lo = __builtin_elementwise_sub_sat(sbs, Q), hi0 = __builtin_elementwise_sub_sat(sbe, Q), hi = hi0 < 4u ? hi0 : 4u;\n"
+              "      if (hi > lo) {\n"
+              "        bm = ~(0xfffffffeu << (8u * hi - 1u)) & (0xffffffffu << (8u * lo));\n")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
