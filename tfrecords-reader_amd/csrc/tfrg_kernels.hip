@@ -1584,7 +1584,9 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
           if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
         }
         if (spec_on && spec_l[k]) {  // (wave-uniform) speculative row split r; irregular records counted
-          if (valid) o.rs[(size_t)k * (B.n + 1) + r] = r;
+          // (the row splits of a final placement are implicit for the first 64 slots:
+          // tfrg_info.placed_slots; a failed placement has them all rewritten by k_down_gather)
+          if (valid && k >= 64u) o.rs[(size_t)k * (B.n + 1) + r] = r;
           const uint64_t irm = __ballot(valid && !(done && c == (1u | kCountInline)));
           if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
         }

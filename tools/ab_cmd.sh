@@ -1,4 +1,3 @@
 export TMPDIR=/tmp; mkdir -p gpurun_out/ab
 timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu tests > gpurun_out/ab/tests.log 2>&1; rc=$?; tail -3 gpurun_out/ab/tests.log; [ $rc = 0 ] || exit 1
-STEPS=100 bash tools/ab.sh c4of8 libtfrg.so libtfrg_nors.so libtfrg.so libtfrg_nors.so || exit 1
-STEPS=20 bash tools/ab.sh c4 libtfrg.so || exit 1
+bash tools/evidence_r04.sh 2
