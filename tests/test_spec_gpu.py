@@ -90,6 +90,26 @@ def test_all_regular_placed():
         assert np.array_equal(np.array(a.row_splits[k]), np.arange(n + 1, dtype=np.uint32)), key
 
 
+def test_placed_slots_reported():
+    """tfrg_info.placed_slots names the slots whose row splits are implicit (never stored on the
+    device, written by the fetch); a slot whose placement failed is not among them and its row
+    splits are the scanned ones."""
+    n = 5000
+    a = _same([_reg(i) for i in range(n)])
+    placed = int(a.info.placed_slots)
+    assert placed != 0
+    for k in range(len(a.slot_key)):
+        if (placed >> k) & 1:
+            assert np.array_equal(np.array(a.row_splits[k]), np.arange(n + 1, dtype=np.uint32)), k
+    pl = [_reg(i) for i in range(n)]
+    pl[777] = example(entry(b"label", i64(3, 4)), entry(b"id", byt(b"x")), entry(b"w", f32(1.0)), entry(b"k", i64(1)))
+    b = _same(pl)
+    kl = [k for k, key in enumerate(b.slot_key) if key == "label"]
+    assert kl and not (int(b.info.placed_slots) >> kl[0]) & 1
+    rs = np.array(b.row_splits[kl[0]]).astype(np.int64)
+    assert rs[778] - rs[777] == 2 and rs[-1] == n + 1
+
+
 def test_c1_batch_placed():
     _same(synth.c1_payloads(20000))
 

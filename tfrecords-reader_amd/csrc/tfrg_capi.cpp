@@ -90,6 +90,8 @@ struct tfrg_ctx {
   DBuf in_bytes, in_start, in_end;
   // arena
   DBuf status, aux, verdict, order, count, loc, rs, slot_base, totals, kind_totals;
+  DBuf ident;            // 0, 1, 2, ... (ident_n words): the fetched row splits of placed slots
+  size_t ident_n = 0;
   DBuf i64, f32, b_off, b_len, big_list, slow_list, miss, info, tsum, crc_rec, crc_base, crc_part;
   DBuf dq, dq_cnt;  // deferred packed-int64 bodies (k_body_count)
   DBuf lmask, rlist;  // k_tpl_lane's per-group miss masks and listed groups
@@ -205,7 +207,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   if (c->last_stream) (void)hipStreamSynchronize(c->last_stream);
   DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
                  &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status, &c->aux, &c->verdict,
-                 &c->order, &c->count, &c->loc, &c->rs, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
+                 &c->order, &c->count, &c->loc, &c->rs, &c->ident, &c->slot_base, &c->totals, &c->kind_totals, &c->i64,
                  &c->f32, &c->b_off, &c->b_len, &c->big_list, &c->slow_list, &c->miss, &c->info, &c->tsum,
                  &c->bdata, &c->boff64, &c->blb, &c->bbig, &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec,
                  &c->dq, &c->dq_cnt, &c->lmask, &c->rlist};
@@ -1005,16 +1007,23 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
   HIP_TRY(cp(h->aux, c->aux.p, n * 8));
   HIP_TRY(cp(h->verdict, c->verdict.p, n));
   HIP_TRY(cp(h->order, c->order.p, S * n * 2));
-  // row splits: a placed slot's are the identity (never stored on the device), written here while
-  // the other rows copy
+  // row splits: a placed slot's are the identity, never stored by the decode; they copy from a
+  // device identity row (filled once per size), as fast as the stored rows and as asynchronous
   if (h->row_splits) {
-    for (size_t k = 0; k < S; ++k) {
-      uint32_t* row = h->row_splits + k * (n + 1);
-      if (k < 64 && ((info.placed_slots >> k) & 1ull)) continue;
-      HIP_TRY(cp(row, c->rs.as<uint32_t>() + k * (n + 1), (n + 1) * 4));
+    if (S && (info.placed_slots & (S >= 64 ? ~0ull : (1ull << S) - 1ull)) && c->ident_n < n + 1) {
+      const size_t m = std::max<size_t>(n + 1, 2 * c->ident_n);
+      std::vector<uint32_t> v(m);
+      std::iota(v.begin(), v.end(), 0u);
+      c->ident_n = 0;
+      HIP_TRY(c->ident.ensure(m * 4));
+      HIP_TRY(hipMemcpy(c->ident.p, v.data(), m * 4, hipMemcpyHostToDevice));
+      c->ident_n = m;
     }
-    for (size_t k = 0; k < S && k < 64; ++k)
-      if ((info.placed_slots >> k) & 1ull) std::iota(h->row_splits + k * (n + 1), h->row_splits + (k + 1) * (n + 1), 0u);
+    for (size_t k = 0; k < S; ++k) {
+      const bool pk = k < 64 && ((info.placed_slots >> k) & 1ull);
+      HIP_TRY(cp(h->row_splits + k * (n + 1), pk ? c->ident.as<uint32_t>() : c->rs.as<uint32_t>() + k * (n + 1),
+                 (n + 1) * 4));
+    }
   }
   HIP_TRY(cp(h->slot_base, c->slot_base.p, S * 8));
   // (clamped to the capacities: a result that overflowed them fails in tfrg_result_info above)
