@@ -25,9 +25,10 @@ struct DevSchema {
   uint32_t tpl_w;              // their window words W (16, 32 or 64)
   // [n_slots] speculative placement of single values (null = off): 0, or (rank + 1) << 2 | kind for
   // a slot that is an inline single value in every learned template, as are all slots of its kind
-  // before it. The lane kernel then writes such a value straight to its column at n * rank + r and
-  // the row split r; k_down_gather skips the slot when every record was regular (irr == 0) and the
-  // slot's column base is n * rank, i.e. when that placement is the final one.
+  // before it. The lane kernel then writes such a value straight to its column at n * rank + r (the
+  // row split r stays implicit for the first 64 slots); k_down_gather skips the slot when every
+  // record was regular (irr == 0) and the slot's column base is n * rank, i.e. when that placement
+  // is the final one (tfrg_info.placed_slots), and writes all its row splits otherwise.
   const uint32_t* spec;
 };
 
