@@ -2422,8 +2422,33 @@ __global__ __launch_bounds__(kSpineBlock) void k_spine(DevOut o, const uint8_t* 
   __shared__ uint8_t s_kind[kSpineBlock];
   const uint32_t lane = threadIdx.x & 63u, wid = threadIdx.x >> 6;
   if (threadIdx.x == 0) s_ticket = atomicAdd(&o.info[kInfoSpineTicket], 1u);
+  // Every slot's placement final (a templated batch): no scan, no look-back and no last-workgroup
+  // pass, since the placement fixes every total (n) and column base. Read beside the ticket: one
+  // round trip to the device-scope words instead of three.
+  const bool allp = spec && n_slots <= (uint32_t)kSpineBlock &&
+                    __syncthreads_and(threadIdx.x >= n_slots || spec_placed(spec, o, threadIdx.x));
   __syncthreads();
   const uint32_t slot = s_ticket / o.n_chunks, chunk = s_ticket % o.n_chunks;
+  if (allp) {  // (workgroup-uniform) this chunk's tile sums zeroed for the next decode
+    uint32_t* t = o.tsum + (size_t)slot * o.tile_stride;
+    const uint32_t i0 = (chunk << kSpineChunkShift) + threadIdx.x * kSpineItems;
+#pragma unroll
+    for (int j = 0; j < kSpineItems; j += 4)
+      if (i0 + j < n_tiles) *reinterpret_cast<uint4*>(t + i0 + j) = make_uint4(0, 0, 0, 0);
+    if (s_ticket == 0u && threadIdx.x == 0) {  // totals, column bases, kind totals (as the last pass)
+      uint64_t acc[4] = {0, 0, 0, 0};
+      for (uint32_t k = 0; k < n_slots; ++k) {
+        const uint32_t kd = slot_kind[k] & 3u;
+        o.totals[k] = n;
+        o.slot_base[k] = acc[kd];
+        acc[kd] += n;
+      }
+      for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+      if (acc[TFRG_KIND_INT64] > o.cap_i64 || acc[TFRG_KIND_FLOAT] > o.cap_f32 || acc[TFRG_KIND_BYTES] > o.cap_b)
+        o.info[kInfoOverflow] = 1u;
+    }
+    return;
+  }
   if (spec_failed(spec, o, slot)) {  // (workgroup-uniform; rare: an irregular batch)
     const uint32_t sw = spec[slot];
     const uint64_t sb = (uint64_t)n * ((sw >> 2) - 1u);

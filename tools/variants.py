@@ -62,6 +62,9 @@ VARIANTS = {
               "      const uint32_t lo = __builtin_elementwise_sub_sat(sbs, Q), hi0 = __builtin_elementwise_sub_sat(sbe, Q), hi = hi0 < 4u ? hi0 : 4u;\n"
               "      if (hi > lo) {\n"
               "        bm = ~(0xfffffffeu << (8u * hi - 1u)) & (0xffffffffu << (8u * lo));\n")],
+    # k_spine without its every-slot-placed fast path (the per-slot fast path and last-workgroup pass)
+    "noallp": [("tfrg_kernels.hip", "  const bool allp = spec && n_slots <= (uint32_t)kSpineBlock &&",
+                "  const bool allp = false && spec && n_slots <= (uint32_t)kSpineBlock &&")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
