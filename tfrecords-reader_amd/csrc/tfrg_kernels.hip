@@ -2683,11 +2683,8 @@ __global__ __launch_bounds__(kLaneBlock) void k_down_gather(DevBatch B, DevSchem
   // slots whose speculative placement by the lane kernel is final (DevSchema::spec): nothing to do.
   // Read once (the first 64 slots as a mask): the tile-sum stores below may alias irr for the
   // compiler, which would otherwise re-load spec / irr with their latency in every group.
-  uint64_t pmask = 0;
-  if (sc.spec)
-    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;
-  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) |
-          __builtin_amdgcn_readfirstlane((uint32_t)pmask);
+  // (lane k: slot k, so the words of all of them are loaded at once)
+  const uint64_t pmask = sc.spec ? (uint64_t)__ballot(lane < S && spec_placed(sc.spec, o, lane)) : 0ull;
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // (for k_tail_gather, which clears irr)
     o.info[kInfoPlacedLo] = (uint32_t)pmask;
     o.info[kInfoPlacedHi] = (uint32_t)(pmask >> 32);

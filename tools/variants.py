@@ -65,6 +65,11 @@ VARIANTS = {
     # k_spine without its every-slot-placed fast path (the per-slot fast path and last-workgroup pass)
     "noallp": [("tfrg_kernels.hip", "  const bool allp = spec && n_slots <= (uint32_t)kSpineBlock &&",
                 "  const bool allp = false && spec && n_slots <= (uint32_t)kSpineBlock &&")],
+    # k_down_gather's placed-slot mask by one thread per workgroup, slot after slot
+    "serialpm": [("tfrg_kernels.hip",
+                  "  const uint64_t pmask = sc.spec ? (uint64_t)__ballot(lane < S && spec_placed(sc.spec, o, lane)) : 0ull;\n",
+                  "  uint64_t pmask = 0;\n  if (sc.spec)\n    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;\n"
+                  "  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)pmask);\n")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
