@@ -17,6 +17,17 @@ def test_header_declares_the_bound_surface():
     assert declared_symbols() == set(N.SIGNATURES)
 
 
+def test_integration_doc_names_only_declared_symbols():
+    """Every tfrg_* call in INTEGRATION.md's code blocks (the bindings a maintainer would copy) is
+    declared in include/tfrg.h: the document cannot point at a removed entry point."""
+    doc = (HEADER.parents[1] / "INTEGRATION.md").read_text()
+    blocks = "\n".join(re.findall(r"```[a-z]*\n(.*?)```", doc, flags=re.S))
+    named = set(re.findall(r"\b(tfrg_[a-z0-9_]+)\s*\(", blocks)) | set(re.findall(r"\blib\.(tfrg_[a-z0-9_]+)", blocks))
+    types = {"tfrg_ctx", "tfrg_columns", "tfrg_info", "tfrg_stream", "tfrg_host_ctx", "tfrg_host_record"}
+    assert named, "no calls found in INTEGRATION.md"
+    assert named - types <= declared_symbols(), sorted(named - types - declared_symbols())
+
+
 def test_library_exports_every_declared_symbol():
     lib = N.lib()
     for name in declared_symbols():
