@@ -61,6 +61,10 @@ def parse_args(argv=None):
                     help="measure one config only and report it as the headline (profiling runs)")
     ap.add_argument("--no-extra", action="store_true", help="skip the per-config measurements at N = 1")
     ap.add_argument("--profile-steps", type=int, default=5)
+    # record offsets handed to the decode: "auto" = u32 ends of back-to-back records (the framing
+    # index of whole files; 4 B per record), else u32 (start, end) pairs; "u64" = the u64 pairs of
+    # tfrg_decode_device (16 B per record)
+    ap.add_argument("--offsets", default="auto", choices=["auto", "u32", "u64"])
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall budget of each CPU baseline")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args(argv)
@@ -224,11 +228,22 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     sd = shard.ShardDecoder(ctx.local, ctx.args.batch_bytes, ctx.args.streams)
     nbytes = int(w.buf.size)
     plan = sd.plan(w.starts, w.ends, nbytes)
-    rst, ren = sd.rebase(plan, w.starts, w.ends)
     d_bytes = torch.zeros(((nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
     d_bytes[:nbytes].copy_(torch.from_numpy(w.buf))
-    d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
-    d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+    omode = ctx.args.offsets
+    if omode == "u64":
+        rst, ren = sd.rebase(plan, w.starts, w.ends)
+        d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
+        d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        off_bytes, firsts = 16, None
+    else:  # per-batch u32 offsets; only the ends when the records lie back to back
+        rst, ren, firsts = sd.rebase32(plan, w.starts, w.ends)
+        if omode == "u32" and rst is None:
+            rst = sd.rebase(plan, w.starts, w.ends)[0].astype(np.uint32)
+        d_st = torch.from_numpy(rst.view(np.int32)).to(dev) if rst is not None else None
+        d_en = torch.from_numpy(ren.view(np.int32)).to(dev)
+        off_bytes = 4 if rst is None else 8
+        omode = "ends" if rst is None else "u32"
     del rst, ren
     if not templates:
         for d in sd._decoders(len(plan)):
@@ -242,7 +257,11 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         d.set_record_bound(max_record)
 
     def step(streams=handles):
-        sd.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(), streams=streams)
+        if off_bytes == 16:
+            sd.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(), streams=streams)
+        else:
+            sd.decode_device32(plan, d_bytes.data_ptr(), d_st.data_ptr() if d_st is not None else None,
+                               d_en.data_ptr(), firsts, streams=streams)
 
     for _ in range(max(1, warmup)):
         step()
@@ -324,7 +343,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     for i in infos:
         placed &= int(i.placed_slots)
     n_placed = bin(placed & ((1 << min(n_slots, 64)) - 1)).count("1")
-    lane_alg = small_bytes + n_small * (16 + 5 + 2 * n_slots + 4 * (n_slots - n_placed)) + 8 * present_small
+    # (off_bytes: the record offsets as handed over -- 4 B of u32 ends, 8 B of u32 pairs, 16 B of u64)
+    lane_alg = small_bytes + n_small * (off_bytes + 5 + 2 * n_slots + 4 * (n_slots - n_placed)) + 8 * present_small
     alg = {
         # template path: its records' framed bytes + offsets in; status, verdict, order per slot, a row
         # split (or count) per slot not placed, and a value / location word per present list out
@@ -333,7 +353,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         "k_lane_count": lane_alg,
         # streaming payload CRC of the records above lane_max (their bytes + list entry and offsets);
         # the exact walker's slow list is empty on these workloads
-        "k_tail_count": big_bytes + 32 * n_big,
+        "k_tail_count": big_bytes + (16 + off_bytes) * n_big,
         "k_spine": 8 * n_slots * n_tiles,
         "k_down_gather": 8 * n * n_slots + vals + 8 * min(n_vals, present_small),
         # out-of-line lists: every value written once (their record bytes are counted by the lanes)
@@ -343,7 +363,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     launches = len(plan)
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
     n_keys = len(sd.keys.keys)
-    R = framed + 16 * n
+    R = framed + off_bytes * n
     # (SURVEY D2's W, less the row splits of placed slots, which are implicit: never stored)
     W = 4 * n + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
     ms_step = elapsed / steps * 1e3
@@ -354,6 +374,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         "framed_bytes": framed,
         "batches": launches,
         "batch_bytes_max": int((plan[:, 3] - plan[:, 2]).max()),
+        "offsets": {"mode": omode, "bytes_per_record": off_bytes},
         "streams": len(handles),
         "ms_per_step": round(ms_step, 4),
         "GiB_s": round(framed / (ms_step / 1e3) / 2**30, 3),

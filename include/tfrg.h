@@ -191,6 +191,14 @@ int tfrg_host_decode(tfrg_host_ctx* ctx, const uint8_t* payload, uint64_t len, u
  * the context's own stream. Results stay valid until the next decode on this context. */
 int tfrg_decode_device(tfrg_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_start,
                        const uint64_t* d_end, uint32_t n, uint32_t flags, void* stream);
+/* Same with 32-bit offsets (a batch is < 4 GiB, so offsets relative to d_bytes fit; the index's
+ * (tfrecord_start, tfrecord_end) of indexer.pyx:212-252 rebased per batch). d_start32 == NULL: the
+ * records lie back to back -- record 0 starts at first_start and record i > 0 where record i - 1
+ * ends, as the framing index of a file image or a gathered selection always gives them -- and
+ * only their u32 ends are read (4 bytes per record instead of 16). Results are those of
+ * tfrg_decode_device on the same ranges. */
+int tfrg_decode_device32(tfrg_ctx* ctx, const uint8_t* d_bytes, uint64_t nbytes, const uint32_t* d_start32,
+                         const uint32_t* d_end32, uint32_t first_start, uint32_t n, uint32_t flags, void* stream);
 /* Same from host memory: stages bytes/start/end into context-owned HBM (H2D on the stream). */
 int tfrg_decode_host(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                      const uint64_t* h_end, uint32_t n, uint32_t flags, void* stream);

@@ -78,11 +78,13 @@ def _shard_rows(sb: shard.ShardBatch, res: shard.ShardResult):
     return out
 
 
-@pytest.mark.parametrize("batch_bytes", [1 << 18, 1 << 20])
-def test_shard_split_over_batches_device_and_host(directory, batch_bytes):
+@pytest.mark.parametrize("batch_bytes,offsets", [(1 << 18, "u64"), (1 << 20, "u64"), (1 << 18, "ends"),
+                                                 (1 << 20, "u32")])
+def test_shard_split_over_batches_device_and_host(directory, batch_bytes, offsets):
     """One rank's shard decoded as several batches (one context each, two streams) from HBM and from
     host memory: the same rows as the single-batch decode of the whole shard, hence the oracle
-    (test above)."""
+    (test above). Device offsets as u64 pairs (tfrg_decode_device), u32 pairs or the u32 ends of
+    back-to-back records alone (tfrg_decode_device32)."""
     import torch
 
     sb = shard.read_shard(directory)
@@ -98,30 +100,73 @@ def test_shard_split_over_batches_device_and_host(directory, batch_bytes):
         assert (plan[1:, 0] == plan[:-1, 1]).all() and plan[0, 0] == 0 and plan[-1, 1] == len(sb)
         host = _shard_rows(sb, sd.decode(sb.buf, sb.starts, sb.ends))
         assert host == whole
-        rst, ren = sd.rebase(plan, sb.starts, sb.ends)
         dev = torch.device("cuda", 0)
         d_bytes = torch.zeros(((sb.nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
         d_bytes[: sb.nbytes].copy_(torch.from_numpy(sb.buf))
-        d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
-        d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        if offsets == "u64":
+            rst, ren = sd.rebase(plan, sb.starts, sb.ends)
+            d_st = torch.from_numpy(rst.view(np.int64)).to(dev)
+            d_en = torch.from_numpy(ren.view(np.int64)).to(dev)
+        else:
+            rst, ren, firsts = sd.rebase32(plan, sb.starts, sb.ends)
+            assert rst is None  # (whole files: back to back)
+            if offsets == "u32":
+                rst = sd.rebase(plan, sb.starts, sb.ends)[0].astype(np.uint32)
+            d_st = torch.from_numpy(rst.view(np.int32)).to(dev) if rst is not None else None
+            d_en = torch.from_numpy(ren.view(np.int32)).to(dev)
         sd2 = shard.ShardDecoder(0, batch_bytes=batch_bytes, n_streams=2)
+
+        def run():
+            ss = [s.cuda_stream for s in streams]
+            if offsets == "u64":
+                sd2.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(), streams=ss)
+            else:
+                sd2.decode_device32(plan, d_bytes.data_ptr(), d_st.data_ptr() if d_st is not None else None,
+                                    d_en.data_ptr(), firsts, streams=ss)
+
         try:
             sd2.learn(plan, sb.buf, sb.starts, sb.ends)
             streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
             for _ in range(2):  # twice: the second decode reuses every context's arena
-                sd2.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(),
-                                  streams=[s.cuda_stream for s in streams])
+                run()
             infos = sd2.infos(plan)
             if any(i.n_miss_records for i in infos):  # keys past the learning sample (the flowers files)
                 sd2.decode(sb.buf, sb.starts, sb.ends)
                 sd2.learn(plan, sb.buf, sb.starts, sb.ends)
-                sd2.decode_device(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(),
-                                  streams=[s.cuda_stream for s in streams])
+                run()
                 infos = sd2.infos(plan)
             assert not any(i.n_miss_records for i in infos)
             dev_rows = _shard_rows(sb, sd2.fetch(plan, sb.buf, sb.starts, sb.ends))
             assert dev_rows == whole
         finally:
             sd2.close()
+    finally:
+        sd.close()
+
+
+def test_rebase32_gaps_keep_the_starts(directory):
+    """A file with trailing bytes (fewer than 8: the reference's indexer ignores them,
+    indexer.pyx:225-249) breaks the back-to-back chain: rebase32 then keeps explicit u32 starts,
+    and a decode through them equals the host decode."""
+    import torch
+
+    imgs = [np.fromfile(p, np.uint8) for p in directory[:3]]
+    imgs[0] = np.concatenate([imgs[0], np.frombuffer(b"\x01\x02\x03", np.uint8)])
+    sb = shard.ShardBatch([f"f{i}" for i in range(3)], imgs)
+    sd = shard.ShardDecoder(0, batch_bytes=1 << 30, n_streams=1)
+    try:
+        plan = sd.plan(sb.starts, sb.ends, sb.nbytes)
+        rst, ren, firsts = sd.rebase32(plan, sb.starts, sb.ends)
+        assert rst is not None and len(plan) == 1
+        whole = _shard_rows(sb, sd.decode(sb.buf, sb.starts, sb.ends))
+        dev = torch.device("cuda", 0)
+        d_bytes = torch.zeros(((sb.nbytes + 15) // 16) * 16 + 16, dtype=torch.uint8, device=dev)
+        d_bytes[: sb.nbytes].copy_(torch.from_numpy(sb.buf))
+        d_st = torch.from_numpy(rst.view(np.int32)).to(dev)
+        d_en = torch.from_numpy(ren.view(np.int32)).to(dev)
+        sd.learn(plan, sb.buf, sb.starts, sb.ends)
+        sd.decode_device32(plan, d_bytes.data_ptr(), d_st.data_ptr(), d_en.data_ptr(), firsts)
+        assert not any(i.n_miss_records or i.n_errors for i in sd.infos(plan))
+        assert _shard_rows(sb, sd.fetch(plan, sb.buf, sb.starts, sb.ends)) == whole
     finally:
         sd.close()

@@ -113,3 +113,25 @@ def test_plan_batches_properties():
         assert ((rs + base) == st).all() and ((re + base) == en).all()
     with pytest.raises(ValueError):
         shard.plan_batches(st[::-1].copy(), en[::-1].copy(), 4096)
+
+
+def test_rebase32_back_to_back_and_gaps():
+    """u32 per-batch offsets (tfrg_decode_device32): ends alone for back-to-back records, explicit
+    starts as soon as one record does not start where the previous one ended."""
+    lens = np.array([59, 58, 59, 4000, 59, 58] * 50, np.uint64)
+    en = np.cumsum(lens)
+    st = en - lens
+    plan = shard.plan_batches(st, en, 4096)
+    assert len(plan) > 3
+    s32, e32, first = shard.ShardDecoder.rebase32(plan, st, en)
+    assert s32 is None
+    rs, re = shard.ShardDecoder.rebase(plan, st, en)
+    assert (e32 == re).all() and (first == rs[plan[:, 0]]).all()
+    st2 = st.copy()
+    st2[7:] += 3  # a gap of 3 bytes before record 7
+    en2 = en.copy()
+    en2[7:] += 3
+    plan2 = shard.plan_batches(st2, en2, 4096)
+    s32, e32, first = shard.ShardDecoder.rebase32(plan2, st2, en2)
+    rs, re = shard.ShardDecoder.rebase(plan2, st2, en2)
+    assert s32 is not None and (s32 == rs).all() and (e32 == re).all()

@@ -21,7 +21,8 @@ from tfr_reader import synth
 # tfrg_internal.h layout
 K_L, K_NE, K_CRCW, K_CHAIN, K_K, K_ABSENT, K_ENT = 0, 1, 2, 3, 4, 5, 8
 K_WIN = K_ENT + 4 * 16
-K_WORDS = K_WIN + 3 * 64
+K_SLOT = K_WIN + 3 * 64
+K_WORDS = K_SLOT + 3 * 16
 
 
 def _tables() -> np.ndarray:
@@ -104,6 +105,13 @@ def _emulate(tpls, W, buf, s, e, lane_max=2048):
                 vals.append((slot, mode, rank, ((e + pos) & 0xFFFFFFFF, ln)))
             else:
                 vals.append((slot, mode, rank, (pos, ln)))
+        # the slot table (k_tpl_lane's stores) restates the entries slot by slot
+        for slot, mode, rank, _ in vals:
+            z0, _, cw = (int(v) for v in tp[K_SLOT + 3 * slot : K_SLOT + 3 * slot + 3])
+            assert (z0 & 0xFF, z0 >> 16) == (mode, rank)
+        ent = {int(tp[K_ENT + 4 * k]) & 0xFF for k in range(int(tp[K_NE]))}
+        for slot in set(range(16)) - ent:
+            assert not tp[K_SLOT + 3 * slot : K_SLOT + 3 * slot + 3].any()  # absent: rank 0, count 0
         return t, vals
     return -1, []
 

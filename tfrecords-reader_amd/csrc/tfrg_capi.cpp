@@ -606,6 +606,12 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
       q[2] = x.ent[e + 2];
       q[3] = pos;
       if (slot < 32) present |= 1u << slot;
+      if (slot < kLeanMaxSlots) {  // the slot table (ranks < 2^16: tpl_derive caps them)
+        uint32_t* z = d + kLtSlot + 3 * slot;
+        z[0] = mode | (b << 8) | (x.ent[e + 1] << 16);
+        z[1] = pos;
+        z[2] = x.ent[e + 2];
+      }
     }
     d[kLtAbsent] = ~present & (S >= kLeanMaxSlots ? 0xffffu : ((1u << S) - 1u));
   }
@@ -691,8 +697,40 @@ extern "C" int tfrg_ctx_set_templates(tfrg_ctx* c, int on) {
   return 0;
 }
 
+// record offsets of one decode call (DevBatch: u64 pairs, u32 pairs, or u32 ends of back-to-back records)
+struct Offsets {
+  const uint64_t* s64 = nullptr;
+  const uint64_t* e64 = nullptr;
+  const uint32_t* s32 = nullptr;
+  const uint32_t* e32 = nullptr;
+  uint32_t first = 0;
+  uint32_t mode = kOffU64;
+};
+
+static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const Offsets& off, uint32_t n,
+                             uint32_t flags, void* stream);
+
 int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint64_t* d_start,
                        const uint64_t* d_end, uint32_t n, uint32_t flags, void* stream) {
+  Offsets off;
+  off.s64 = d_start;
+  off.e64 = d_end;
+  return decode_device_any(c, d_bytes, nbytes, off, n, flags, stream);
+}
+
+int tfrg_decode_device32(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const uint32_t* d_start32,
+                         const uint32_t* d_end32, uint32_t first_start, uint32_t n, uint32_t flags, void* stream) {
+  if (n && !d_end32) return TFRG_E_ARG;
+  Offsets off;
+  off.s32 = d_start32;
+  off.e32 = d_end32;
+  off.first = first_start;
+  off.mode = d_start32 ? kOffU32 : kOffEnds;
+  return decode_device_any(c, d_bytes, nbytes, off, n, flags, stream);
+}
+
+static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const Offsets& off, uint32_t n,
+                             uint32_t flags, void* stream) {
   if (!c) return TFRG_E_ARG;
   if (nbytes >= (1ull << 32)) {
     set_error("batch larger than 4 GiB: split it");
@@ -784,8 +822,12 @@ int tfrg_decode_device(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, con
   DevBatch b;
   b.bytes = d_bytes;
   b.nbytes = nbytes;
-  b.start = d_start;
-  b.end = d_end;
+  b.start = off.s64;
+  b.end = off.e64;
+  b.start32 = off.s32;
+  b.end32 = off.e32;
+  b.first = off.first;
+  b.omode = off.mode;
   b.n = n;
   b.flags = flags;
   DevOut o;

@@ -49,12 +49,16 @@ struct DevSchema {
 // [kLtEnt + 4 e] entries {slot | mode << 8 | spec << 12 | len << 16, rank, count word, pos}; mode 0:
 // list location (pos = payload offset, len), 1: inline int64 varint of len bytes at window byte pos,
 // 2: inline float at window byte pos, 3: inline bytes element of len bytes, pos = payload offset -
-// 4 - L (the element's batch offset is end + pos); [kLtWin, +W) Bm, [+W, +2W) Mm, [+2W, +3W) Cm.
+// 4 - L (the element's batch offset is end + pos); [kLtWin, +W) Bm, [+W, +2W) Mm, [+2W, +3W) Cm;
+// [kLtSlot + 3 k] the same entries by SLOT k (< kLeanMaxSlots), so that k_tpl_lane stores slot k's
+// columns once for the lanes of every template: {mode | len << 8 | rank << 16 (0: absent), pos,
+// count word (0: absent)}.
 constexpr uint32_t kTplMaxL = 240, kTplMaxEntries = 16, kTplMax = 4;
 constexpr uint32_t kLtMaxW = 64;
-constexpr uint32_t kLtL = 0, kLtNe = 1, kLtCrcw = 2, kLtChain = 3, kLtK = 4, kLtAbsent = 5, kLtEnt = 8,
-                   kLtWin = kLtEnt + 4 * kTplMaxEntries, kLtWords = kLtWin + 3 * kLtMaxW;
 constexpr uint32_t kLeanMaxSlots = 16;  // k_tpl_lane runs for schemas of at most this many slots
+constexpr uint32_t kLtL = 0, kLtNe = 1, kLtCrcw = 2, kLtChain = 3, kLtK = 4, kLtAbsent = 5, kLtEnt = 8,
+                   kLtWin = kLtEnt + 4 * kTplMaxEntries, kLtSlot = kLtWin + 3 * kLtMaxW,
+                   kLtWords = kLtSlot + 3 * kLeanMaxSlots;
 constexpr uint32_t kLeanTabOff = 51200;  // crc_tab words: T_d, d < 32, 256 entries each (slice-by-32)
 
 // Column targets of one slot for k_tpl_lane, computed on the host per decode.
@@ -75,7 +79,8 @@ struct LeanArgs {
   uint32_t* tsum;  // tile sums, slot k's at k * tile_stride
   uint32_t n_slots;
   uint32_t tile_stride;
-  uint32_t half;   // (launch_tpl_lane) a wave takes half a tile: small batches, twice the waves
+  uint32_t gpw;    // (launch_tpl_lane) 64-record groups per wave: 2 (half a tile: small batches,
+                   // twice the waves, tile sums added atomically) or a multiple of 4 (whole tiles)
   LeanTgt tg[kLeanMaxSlots];
 };
 
@@ -106,14 +111,33 @@ __host__ __device__ inline uint32_t key_hash_words(uint32_t n, uint32_t w0, uint
   return h ^ (h >> 15);
 }
 
+// Record offsets of a batch (tfrg_decode_device: u64 pairs; tfrg_decode_device32: u32 pairs, or u32
+// ends alone for back-to-back records, record r > 0 starting where record r - 1 ends)
+enum OffMode : uint32_t { kOffU64 = 0, kOffU32 = 1, kOffEnds = 2 };
+
 struct DevBatch {
   const uint8_t* bytes;        // records (framed or bare payloads); readable to round_up(nbytes,16)
   uint64_t nbytes;
-  const uint64_t* start;       // [n] absolute offsets into bytes
+  const uint64_t* start;       // [n] absolute offsets into bytes (kOffU64)
   const uint64_t* end;         // [n]
+  const uint32_t* start32;     // [n] (kOffU32)
+  const uint32_t* end32;       // [n] (kOffU32, kOffEnds)
+  uint32_t first;              // kOffEnds: start of record 0
+  uint32_t omode;              // OffMode
   uint32_t n;
   uint32_t flags;
 };
+
+#if defined(__HIPCC__)
+__device__ __forceinline__ uint64_t rec_end(const DevBatch& B, uint32_t r) {
+  return B.omode == kOffU64 ? B.end[r] : (uint64_t)B.end32[r];
+}
+__device__ __forceinline__ uint64_t rec_start(const DevBatch& B, uint32_t r) {
+  if (B.omode == kOffU64) return B.start[r];
+  if (B.omode == kOffU32) return B.start32[r];
+  return r ? (uint64_t)B.end32[r - 1] : (uint64_t)B.first;
+}
+#endif
 
 // Info counters (device, zero at the start of every decode: the previous decode's k_lane_count
 // zeroes the slot the next one uses, DevOut::info_next)

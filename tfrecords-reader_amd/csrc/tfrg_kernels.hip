@@ -516,7 +516,7 @@ __device__ __forceinline__ RecView rec_view_se(const DevBatch& B, uint64_t st, u
 }
 
 __device__ __forceinline__ RecView rec_view(const DevBatch& B, uint32_t r) {
-  return rec_view_se(B, B.start[r], B.end[r]);
+  return rec_view_se(B, rec_start(B, r), rec_end(B, r));
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1425,8 +1425,8 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   // the critical path of the next group)
   uint64_t nst = 0, nen = 0;
   if (more && base + lane < B.n) {
-    nst = B.start[base + lane];
-    nen = B.end[base + lane];
+    nst = rec_start(B, (uint32_t)(base + lane));
+    nen = rec_end(B, (uint32_t)(base + lane));
   }
   while (more) {
     PHASE_MARK(p0);
@@ -1438,8 +1438,8 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     g += nw;
     more = group(g, base, gmask);
     if (more && base + lane < B.n) {
-      nst = B.start[base + lane];
-      nen = B.end[base + lane];
+      nst = rec_start(B, (uint32_t)(base + lane));
+      nen = rec_end(B, (uint32_t)(base + lane));
     }
     RecView v{};
     bool mine = false;
@@ -3247,13 +3247,13 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
   uint32_t i = w0;
   RecPipe q;
   q.r1 = i < nbig ? o.big_list[i] : 0u;
-  q.s1 = B.start[q.r1];
-  q.e1 = B.end[q.r1];
+  q.s1 = rec_start(B, q.r1);
+  q.e1 = rec_end(B, q.r1);
   q.t1 = i < nbig ? o.status[q.r1] : -1;
   Pref pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
   q.r2 = i + stride < nbig ? o.big_list[i + stride] : 0u;
-  q.s2v = B.start[vgpr_launder(q.r2)];
-  q.e2v = B.end[vgpr_launder(q.r2)];
+  q.s2v = rec_start(B, vgpr_launder(q.r2));
+  q.e2v = rec_end(B, vgpr_launder(q.r2));
   q.t2v = o.status[vgpr_launder(q.r2)];
   q.r3v = o.big_list[vgpr_launder(i + 2 * stride < nbig ? i + 2 * stride : 0u)];
   // per-slot constants, and the slot metadata of the NEXT record loaded one record ahead (its
@@ -3296,8 +3296,8 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     q.r2 = rfl32(q.r3v);
     q.r3v = o.big_list[vgpr_launder(i + 3 * stride < nbig ? i + 3 * stride : 0u)];
     pf = pref_load_v(B.bytes, q.s1 & ~15ull, q.t1 == TFRG_OK ? (q.e1 < B.nbytes ? q.e1 : B.nbytes) : 0ull, lane);
-    q.s2v = B.start[vgpr_launder(q.r2)];
-    q.e2v = B.end[vgpr_launder(q.r2)];
+    q.s2v = rec_start(B, vgpr_launder(q.r2));
+    q.e2v = rec_end(B, vgpr_launder(q.r2));
     q.t2v = o.status[vgpr_launder(q.r2)];
     meta_load(q.r1, q.t1 == TFRG_OK);
     if (!ok) continue;  // wave-uniform

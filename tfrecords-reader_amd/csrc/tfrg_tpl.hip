@@ -13,8 +13,12 @@
 //   * CRC: one LDS lookup per variable payload byte in the position tables T_d (d = the byte's
 //     distance from the payload end, slice-by-32 tables), XOR-combined; variable bits further than
 //     32 bytes from the end first run a slice-by-4 chain whose state joins at distance 28..31;
-//   * the template's dict straight into the columns: order, count / loc, or the speculatively
-//     placed value + row split (DevSchema::spec), and the per-tile value counts.
+//   * the dict into the columns, ONE store per column and 64-record group whatever template each
+//     lane took: per slot, every template with hits in the group contributes its lanes' order,
+//     count / loc or speculatively placed value (DevSchema::spec; the row split r implicit), taken
+//     from the window registers at the template's (wave-uniform) position, and a select keeps each
+//     lane's own; then the per-tile value counts.
+// A wave owns a contiguous range of groups (whole tiles, or half a tile on small batches).
 // A record no template takes (another shape, a framing or CRC mismatch) is left to k_lane_count:
 // per 64-record group a miss mask (DevOut::lmask) and a list of the groups with misses
 // (DevOut::rlist).
@@ -81,10 +85,17 @@ __device__ __forceinline__ uint32_t bytes_mask(uint32_t nb) { return nb >= 4u ? 
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-template <int W>
+// record offsets of one lane (u32: the lean path runs on batches < 4 GiB); for kOffEnds, s is lane
+// 0's start only (the previous record's end), the other lanes take theirs from lane - 1 (start_of)
+struct LaneOff {
+  uint32_t s, e;
+};
+
+template <int W, int OM>
 __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_tpl_lane(
     DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ tpl, const uint32_t* __restrict__ tabs) {
   static_assert(W == 16 || W == 32 || W == 64, "window words");
+  typedef uint32_t wvec __attribute__((ext_vector_type(W)));
   __shared__ uint32_t tab[kTplTabs * 256];
   for (uint32_t i = threadIdx.x; i < kTplTabs * 256; i += kTplBlock) tab[i] = tabs[i];
   __syncthreads();
@@ -93,35 +104,46 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   // batches are < 0xffffff00 bytes (launch_tpl_lane): an offset of 0xffffff00 reads zeros
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)B.nbytes, 0x00020000);
+  const uint32_t nb = (uint32_t)B.nbytes;
   const uint32_t ngroups = (B.n + 63u) >> 6;
-  // A wave takes whole 256-record tiles (4 groups of 64), tile t0 + k nw: the per-slot tile sums
-  // are then one plain store per tile (lane k: slot k), no atomics. kTileShift = 8 (asserted below).
   static_assert(kTileShift == 8, "4 groups of 64 records per tile");
-  const uint32_t ntiles = (ngroups + 3u) >> 2;
-  const uint32_t nw = gridDim.x * kWaves;
-  // (A.half: wave w takes the groups 2w, 2w + 1, one step, and adds its tile sums atomically: a
-  // batch too small to give every CU a workgroup runs on twice the waves)
-  const uint32_t w0 = blockIdx.x * kWaves + wib;
-  const uint32_t t0 = A.half ? w0 >> 1 : w0;
-  if (t0 >= ntiles || (A.half && 4u * t0 + ((w0 & 1u) << 1) >= ngroups)) return;  // (wave-uniform; no barrier follows)
-  // Two groups per step (g, g + 1 of the wave's tile), their windows loaded together: a step waits
-  // once, for both windows and the previous step's column stores (gfx9 counts stores in vmcnt, in
-  // issue order), so each wait covers 128 records. The offsets of the next step are requested
-  // before this step's stores (they are then ready without waiting for those).
-  auto offsets = [&](uint32_t gg, uint64_t& s, uint64_t& e) {
-    s = 0;
-    e = 0;
-    if (gg < ngroups && (gg << 6) + lane < B.n) {
-      s = B.start[(gg << 6) + lane];
-      e = B.end[(gg << 6) + lane];
+  // the wave's groups [gbeg, gend): whole tiles (gpw a multiple of 4, tile sums stored) or half a
+  // tile (gpw 2: small batches on twice the waves, tile sums added atomically)
+  const uint32_t gpw = A.gpw;
+  const uint32_t gbeg = (blockIdx.x * kWaves + wib) * gpw;
+  if (gbeg >= ngroups) return;  // (wave-uniform; no barrier follows)
+  const uint32_t gend = gbeg + gpw < ngroups ? gbeg + gpw : ngroups;
+  const bool whole = (gpw & 3u) == 0u;
+
+  auto offsets = [&](uint32_t g) -> LaneOff {
+    LaneOff f{1u, 0u};  // (s > e: not in the batch)
+    const uint32_t r = (g << 6) + lane;
+    if (g < gend && r < B.n) {
+      if constexpr (OM == kOffU64) {
+        const uint64_t s = B.start[r], e = B.end[r];
+        if (((s | e) >> 32) == 0) f = LaneOff{(uint32_t)s, (uint32_t)e};  // (else k_lane_count's record)
+      } else if constexpr (OM == kOffU32) {
+        f = LaneOff{B.start32[r], B.end32[r]};
+      } else {
+        f.e = B.end32[r];
+        f.s = lane ? 0u : (r ? B.end32[r - 1] : B.first);
+      }
     }
+    return f;
   };
-  auto in_batch = [&](uint32_t gg, uint64_t s, uint64_t e) {
-    return gg < ngroups && (gg << 6) + lane < B.n && s <= e && e <= B.nbytes && e >= 16u;
+  auto start_of = [&](const LaneOff& f) -> uint32_t {
+    if constexpr (OM == kOffEnds)  // wave_shr:1 -- lane l > 0 reads lane l - 1's end; lane 0 keeps its own
+      return (uint32_t)__builtin_amdgcn_update_dpp((int)f.s, (int)f.e, 0x138, 0xf, 0xf, false);
+    else
+      return f.s;
   };
-  auto window = [&](uint32_t (&wn)[W], bool inb, uint64_t e, uint32_t gg) {
-    const bool full = inb && e >= 4u * W;
-    const uint32_t voff = full ? (uint32_t)e - 4u * W : 0xffffff00u;
+  auto in_batch = [&](uint32_t g, uint32_t s, uint32_t e) {
+    return (g << 6) + lane < B.n && s <= e && e <= nb && e >= 16u;
+  };
+  auto window = [&](wvec& wn, const LaneOff& f, uint32_t g) {
+    const uint32_t e = f.e;
+    const bool full = e >= 4u * W && e <= nb;
+    const uint32_t voff = full ? e - 4u * W : 0xffffff00u;
 #pragma unroll
     for (int q = 0; q < W / 4; ++q) {
       const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, voff + 16u * q, 0, 0));
@@ -132,34 +154,51 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
     // a record ending in the batch's first 4 W bytes (group 0 only): its window begins before the
     // batch; those bytes are outside the record (template mask 0), the rest is read byte by byte
-    const bool head = inb && !full;
-    if (gg == 0u && __ballot(head)) {
+    if (g == 0u) {
+      const bool head = in_batch(g, start_of(f), e) && !full;
+      if (__ballot(head)) {
 #pragma unroll
-      for (int i = 0; i < W; ++i) {
-        uint32_t x = 0;
+        for (int i = 0; i < W; ++i) {
+          uint32_t x = 0;
 #pragma unroll
-        for (int b = 0; b < 4; ++b) {
-          const int64_t p = (int64_t)e - 4 * W + 4 * i + b;
-          if (head && p >= 0) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0) << (8 * b);
+          for (int b = 0; b < 4; ++b) {
+            const int64_t p = (int64_t)e - 4 * W + 4 * i + b;
+            if (head && p >= 0) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0) << (8 * b);
+          }
+          if (head) wn[i] = x;
         }
-        if (head) wn[i] = x;
       }
     }
   };
+  // window word q (wave-uniform): one indexed move (s_set_gpr_idx) for W <= 32; a compare chain for
+  // W = 64, whose 64-register vector the indexed form would move through scratch
+  auto wsel = [](const wvec& w, uint32_t q) -> uint32_t {
+    if constexpr (W <= 32) {
+      return w[q & (W - 1u)];
+    } else {
+      uint32_t a = 0;
+#pragma unroll
+      for (int i = 0; i < W; ++i)
+        if (q == (uint32_t)i) a = w[i];
+      return a;
+    }
+  };
   uint32_t acc = 0;  // lane k: slot k's value count over this tile's records so far
-  // one group: template match + CRC, the template's dict into the columns, the miss mask
-  auto proc = [&](const uint32_t (&w)[W], uint32_t g, uint64_t st, uint64_t en) {
+  // one group: template match + CRC (-> tsel, the lane's template), then the dict into the columns
+  auto proc = [&](const wvec& w, uint32_t g, const LaneOff& f) {
     const uint32_t r = (g << 6) + lane;
     const bool valid = r < B.n;
+    const uint32_t st = start_of(f), en = f.e;
     const bool inb = in_batch(g, st, en);
-    const uint32_t en32 = (uint32_t)en;
-    const uint32_t rl = (uint32_t)(en - st);
-    bool hit = false;
+    const uint32_t rl = en - st;
+    uint32_t tsel = kTplMax;  // (none)
+    uint32_t hmask = 0;       // templates with hits (wave-uniform)
+    uint32_t hcnt = 0;        // their hit counts, 8 bits each (wave-uniform)
     for (uint32_t t = 0; t < A.n_tpl; ++t) {  // (wave-uniform)
       cu32* tp = (cu32*)tpl + t * kLtWords;
       const uint32_t L = tp[kLtL];
       if (L + 16u > A.lane_max) continue;  // (its records belong to the wavefront kernels)
-      const bool cand = inb && !hit && rl == L + 16u;
+      const bool cand = inb && tsel == kTplMax && rl == L + 16u;
       if (!__ballot(cand)) continue;
       uint32_t diff = 0;
 #pragma unroll
@@ -182,41 +221,46 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
 #undef TFRG_LIN
       const bool ok = cand && diff == 0u && crc_mask(lin ^ tp[kLtK]) == w[W - 1];
       const uint64_t okm = __ballot(ok);
-      hit |= ok;
       if (!okm) continue;
-      // the template's dict, for the lanes that took it
-      if (ok) {
-        o.status[r] = TFRG_OK;
-        o.verdict[r] = (uint8_t)kHitVerdict;
-      }
-      const uint32_t hits = (uint32_t)__popcll(okm);
-      const uint32_t ne = tp[kLtNe];
-      for (uint32_t e = 0; e < ne; ++e) {  // (wave-uniform)
-        const uint32_t e0 = tp[kLtEnt + 4 * e], rank = tp[kLtEnt + 4 * e + 1], cw = tp[kLtEnt + 4 * e + 2],
-                       pos = tp[kLtEnt + 4 * e + 3];
-        const uint32_t slot = e0 & 0xffu, mode = (e0 >> 8) & 0xfu, len = e0 >> 16;
-        const LeanTgt& T = A.tg[slot];
-        uint32_t lx, ly = 0;
-        if (mode == 1u || mode == 2u) {  // one int64 varint / one float: the 4 bytes at window byte pos
-          // (from the window's registers: a load here would wait out every store before it, vmcnt)
-          const uint32_t q = pos >> 2;
-          uint32_t a = 0, b = 0;
-#pragma unroll
-          for (int i = 0; i < W; ++i)
-            if (q == (uint32_t)i) {  // (wave-uniform)
-              a = w[i];
-              b = i + 1 < W ? w[i + 1] : 0u;
-            }
-          const uint32_t x = __builtin_amdgcn_alignbyte(b, a, pos & 3u);
-          lx = mode == 1u ? vgroups(x, bytes_mask(len)) : x;
-        } else if (mode == 3u) {  // one bytes element: its batch offset and length
-          lx = en32 + pos;
-          ly = len;
-        } else {  // a list: its payload-relative location
-          lx = pos;
-          ly = len;
+      tsel = ok ? t : tsel;
+      hmask |= 1u << t;
+      hcnt |= (uint32_t)__popcll(okm) << (8u * t);
+    }
+    const bool hit = tsel != kTplMax;
+    if (hit) {
+      o.status[r] = TFRG_OK;
+      o.verdict[r] = (uint8_t)kHitVerdict;
+    }
+    if (hmask) {
+      // per slot: each template with hits gives its lanes' order, count word and value / location,
+      // read from its slot table (wave-uniform) and, for inline values, from the window registers
+      for (uint32_t k = 0; k < A.n_slots; ++k) {  // (wave-uniform)
+        uint32_t rank = 0, cw = 0, lx = 0, ly = 0, tot = 0;
+        for (uint32_t m = hmask; m; m &= m - 1u) {  // (wave-uniform)
+          const uint32_t t = __builtin_ctz(m);
+          cu32* z = (cu32*)tpl + t * kLtWords + kLtSlot + 3u * k;
+          const uint32_t z0 = z[0], pos = z[1], cwt = z[2];
+          const uint32_t mode = z0 & 0xffu, len = (z0 >> 8) & 0xffu;
+          uint32_t vx = pos, vy = len;  // mode 0: a list's payload-relative location (absent: 0, 0)
+          if (mode == 1u || mode == 2u) {  // one int64 varint / one float: the 4 bytes at window byte pos
+            // (from the window registers, by a wave-uniform register index: a load here would wait
+            // out every store before it, vmcnt)
+            const uint32_t q = pos >> 2;
+            const uint32_t x = __builtin_amdgcn_alignbyte(wsel(w, q + 1u), wsel(w, q), pos & 3u);
+            vx = mode == 1u ? vgroups(x, bytes_mask(len)) : x;
+            vy = 0;
+          } else if (mode == 3u) {  // one bytes element: its batch offset and length
+            vx = en + pos;
+          }
+          const bool sel = tsel == t;
+          rank = sel ? z0 >> 16 : rank;
+          cw = sel ? cwt : cw;
+          lx = sel ? vx : lx;
+          ly = sel ? vy : ly;
+          tot += (cwt & ~kCountInline) * ((hcnt >> (8u * t)) & 0xffu);
         }
-        if (ok) {
+        const LeanTgt& T = A.tg[k];
+        if (hit) {
           T.ord[r] = (uint16_t)rank;
           if (T.kind) {  // speculative placement: value at column row r; the row split r is implicit
                          // (tfrg_info.placed_slots: a final placement's row splits are never stored)
@@ -233,14 +277,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
             T.loc[r] = make_uint2(lx, ly);
           }
         }
-        acc += lane == slot ? (cw & ~kCountInline) * hits : 0u;
-      }
-      for (uint32_t m = tp[kLtAbsent]; m; m &= m - 1u) {  // slots the shape lacks: order / count 0
-        const LeanTgt& T = A.tg[__builtin_ctz(m)];
-        if (ok) {
-          T.ord[r] = 0;
-          T.cnt[r] = 0;
-        }
+        acc += lane == k ? tot : 0u;
       }
     }
     // records no template took: k_lane_count's
@@ -250,36 +287,34 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       if (mm) o.rlist[atomicAdd(&o.info[kInfoResid], 1u)] = g;
     }
   };
-  // the wave's steps: tile t0 + k nw, groups (4t, 4t+1), (4t+2, 4t+3)
-  uint32_t t = t0, p = A.half ? (w0 & 1u) << 1 : 0u;
-  uint64_t s0, e0, s1, e1;
-  offsets(4u * t + p, s0, e0);
-  offsets(4u * t + p + 1u, s1, e1);
-  while (t < ntiles) {
-    const uint32_t ga = 4u * t + p, gb = ga + 1u;
-    uint32_t wa[W], wb[W];
-    window(wa, in_batch(ga, s0, e0), e0, ga);
-    window(wb, in_batch(gb, s1, e1), e1, gb);
-    const uint64_t sa = s0, ea = e0, sb = s1, eb = e1;
-    // the next step's offsets
-    const uint32_t tn = p ? t + nw : t, pn = p ^ 2u;
-    offsets(4u * tn + pn, s0, e0);
-    offsets(4u * tn + pn + 1u, s1, e1);
-    proc(wa, ga, sa, ea);
-    if (gb < ngroups) proc(wb, gb, sb, eb);
-    // the tile's sums: the first writer of tsum (zero before the decode; k_lane_count's residual
-    // records add theirs with atomics after this kernel)
-    if (A.half) {  // (wave-uniform) the other half of the tile is another wave's
-      if (lane < A.n_slots && acc) atomicAdd(&A.tsum[lane * A.tile_stride + t], acc);
-      break;
+  // two groups per step, their windows loaded together: a step waits once, for both windows and
+  // the previous step's column stores (gfx9 counts stores in vmcnt, in issue order), so each wait
+  // covers 128 records; the next step's offsets are requested before this step's stores (they are
+  // then ready without waiting for those)
+  auto flush = [&](uint32_t g) {  // the tile sums of group g's tile: the first writer of tsum (zero
+    // before the decode; k_lane_count's residual records add theirs with atomics after this kernel)
+    if (lane < A.n_slots && acc) {
+      if (whole)
+        A.tsum[lane * A.tile_stride + (g >> 2)] = acc;
+      else
+        atomicAdd(&A.tsum[lane * A.tile_stride + (g >> 2)], acc);
     }
-    if (p || gb + 1u >= ngroups) {
-      if (lane < A.n_slots && acc) A.tsum[lane * A.tile_stride + t] = acc;
-      acc = 0;
+    acc = 0;
+  };
+  LaneOff f0 = offsets(gbeg), f1 = offsets(gbeg + 1u);
+  for (uint32_t g = gbeg; g < gend; g += 2u) {
+    wvec wa, wb;
+    window(wa, f0, g);
+    window(wb, f1, g + 1u);
+    const LaneOff fa = f0, fb = f1;
+    f0 = offsets(g + 2u);
+    f1 = offsets(g + 3u);
+    proc(wa, g, fa);
+    if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);  // (gpw 2 / a batch's last group)
+    if (g + 1u < gend) {
+      proc(wb, g + 1u, fb);
+      if (((g + 2u) & 3u) == 0u || g + 2u >= gend) flush(g + 1u);
     }
-    if (gb + 1u >= ngroups) break;
-    t = tn;
-    p = pn;
   }
 }
 
@@ -290,21 +325,31 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   const uint32_t groups = (b.n + 63u) / 64u;
   const uint32_t tiles = (groups + 3u) / 4u;  // (one wave per 256-record tile)
   const uint32_t need = (tiles + kTplBlock / 64 - 1) / (kTplBlock / 64);
-  // two tiles per wave (one for batches of fewer than 8 workgroups per CU), no resident-grid
-  // stride: workgroups retire all through the launch, so the end of the batch does not wait on
-  // the waves that drew an extra round of tiles (c4of8: 0.414 ms against 0.430 ms for one round of
-  // resident workgroups; the 32 KiB table copy per workgroup is L2 traffic)
-  const uint32_t per_wave = need >= 8u * (uint32_t)num_cus ? 2u : 1u;
+  // two tiles per wave (one for batches of fewer than 8 workgroups per CU, half a tile for batches of
+  // fewer workgroups than CUs), no resident-grid stride: workgroups retire all through the launch,
+  // so the end of the batch does not wait on the waves that drew an extra round of tiles (c4of8:
+  // 0.414 ms against 0.430 ms for one round of resident workgroups; the 32 KiB table copy per
+  // workgroup is L2 traffic)
   LeanArgs a2 = a;
-  a2.half = need < (uint32_t)num_cus ? 1u : 0u;  // (fewer workgroups than CUs: half a tile per wave)
-  const dim3 grid(a2.half ? (tiles * 2u + kTplBlock / 64 - 1) / (kTplBlock / 64) : need ? (need + per_wave - 1u) / per_wave : 1u);
+  a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;
+  const uint32_t waves = (groups + a2.gpw - 1u) / a2.gpw;
+  const dim3 grid(waves ? (waves + kTplBlock / 64 - 1) / (kTplBlock / 64) : 1u);
   const uint32_t* tabs = d_tab + kLeanTabOff;
+#define TFRG_TPL_LAUNCH(WW, OO) hipLaunchKernelGGL((k_tpl_lane<WW, OO>), grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs)
+#define TFRG_TPL_OM(WW)                                                        \
+  switch (b.omode) {                                                           \
+    case kOffU64: TFRG_TPL_LAUNCH(WW, kOffU64); break;                         \
+    case kOffU32: TFRG_TPL_LAUNCH(WW, kOffU32); break;                         \
+    default: TFRG_TPL_LAUNCH(WW, kOffEnds); break;                             \
+  }
   switch (w) {
-    case 16: hipLaunchKernelGGL(k_tpl_lane<16>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
-    case 32: hipLaunchKernelGGL(k_tpl_lane<32>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
-    case 64: hipLaunchKernelGGL(k_tpl_lane<64>, grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs); break;
+    case 16: TFRG_TPL_OM(16) break;
+    case 32: TFRG_TPL_OM(32) break;
+    case 64: TFRG_TPL_OM(64) break;
     default: return hipErrorInvalidValue;
   }
+#undef TFRG_TPL_OM
+#undef TFRG_TPL_LAUNCH
   return hipGetLastError();
 }
 

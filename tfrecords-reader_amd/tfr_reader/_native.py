@@ -135,6 +135,11 @@ SIGNATURES: dict[str, tuple] = {
         C.c_int,
         [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p],
     ),
+    "tfrg_decode_device32": (
+        C.c_int,
+        [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+         C.c_void_p],
+    ),
     "tfrg_decode_host": (
         C.c_int,
         [C.c_void_p, C.c_void_p, C.c_uint64, u64p, u64p, C.c_uint32, C.c_uint32, C.c_void_p],

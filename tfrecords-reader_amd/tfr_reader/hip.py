@@ -316,6 +316,21 @@ class HipDecoder:
             "tfrg_decode_device",
         )
 
+    def decode_device32(self, d_bytes: int, nbytes: int, d_start32: int | None, d_end32: int, first_start: int,
+                        n: int, *, payload_only: bool = False, crc: bool = True, stream: int | None = None,
+                        strict_crc: bool = False, materialize_bytes: bool = False) -> None:
+        """``decode_device`` with u32 offsets; ``d_start32`` None: back-to-back records, record 0 at
+        ``first_start`` and record i > 0 where record i - 1 ends (only the u32 ends are read)."""
+        self.push_schema()
+        N.check(
+            self._lib.tfrg_decode_device32(
+                self._ctx, C.c_void_p(d_bytes), nbytes, C.c_void_p(d_start32) if d_start32 else None,
+                C.c_void_p(d_end32), first_start, n,
+                self._flags(payload_only, crc, strict_crc, materialize_bytes), C.c_void_p(stream) if stream else None,
+            ),
+            "tfrg_decode_device32",
+        )
+
     def _fetch(self, buf, st, en, info: N.TfrgInfo, payload_only: bool, materialize: bool = False) -> BatchResult:
         n, ns = info.n_records, info.n_slots
         kt = info.kind_totals

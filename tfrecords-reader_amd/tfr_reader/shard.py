@@ -246,6 +246,23 @@ class ShardDecoder:
         base = np.repeat(plan[:, 2].astype(np.uint64), (plan[:, 1] - plan[:, 0]).astype(np.int64))
         return st - base, en - base
 
+    @classmethod
+    def rebase32(cls, plan: np.ndarray, starts, ends) -> tuple[np.ndarray | None, np.ndarray, np.ndarray]:
+        """u32 per-batch offsets for ``decode_device32``: (starts32 or None, ends32, first start of
+        each batch). starts32 is None when the records of every batch lie back to back (record r
+        starts where record r - 1 ends), as the framing index of files without trailing bytes
+        gives them: only the 4-byte ends are then uploaded and read."""
+        st, en = cls.rebase(plan, starts, ends)
+        if st.size and max(int(st.max()), int(en.max())) >= 1 << 32:
+            raise ValueError("a batch spans 4 GiB or more: plan smaller batches")
+        first = st[plan[:, 0].astype(np.int64)] if len(plan) else np.zeros(0, np.uint64)
+        back_to_back = np.ones(st.shape[0], bool)
+        if st.size > 1:
+            back_to_back[1:] = st[1:] == en[:-1]
+        back_to_back[plan[:, 0].astype(np.int64)] = True  # (a batch's first record: first_start)
+        st32 = None if back_to_back.all() else st.astype(np.uint32)
+        return st32, en.astype(np.uint32), first.astype(np.uint32)
+
     def learn(self, plan: np.ndarray, buf: np.ndarray, starts, ends, sample: int = 4096) -> None:
         """Key table and record-shape templates of every batch context from a host sample of the
         first records (device-only callers; the host path learns them itself)."""
@@ -274,6 +291,19 @@ class ShardDecoder:
         for k, (r0, r1, lo, hi) in enumerate(plan.tolist()):
             s = streams[k % len(streams)] if streams else None
             decs[k].decode_device(d_bytes + lo, hi - lo, d_start + 8 * r0, d_end + 8 * r0, r1 - r0, stream=s, **kw)
+
+    def decode_device32(self, plan: np.ndarray, d_bytes: int, d_start32: int | None, d_end32: int, firsts,
+                        streams=None, max_record: int | None = None, **kw) -> None:
+        """``decode_device`` with the u32 offsets of ``rebase32`` (device arrays; ``d_start32`` None
+        for back-to-back records, ``firsts`` the first start of every batch)."""
+        decs = self._decoders(len(plan))
+        if max_record is not None:
+            for d in decs:
+                d.set_record_bound(max_record)
+        for k, (r0, r1, lo, hi) in enumerate(plan.tolist()):
+            s = streams[k % len(streams)] if streams else None
+            decs[k].decode_device32(d_bytes + lo, hi - lo, d_start32 + 4 * r0 if d_start32 else None, d_end32 + 4 * r0,
+                                    int(firsts[k]), r1 - r0, stream=s, **kw)
 
     def infos(self, plan: np.ndarray) -> list:
         """Decode summaries of the last ``decode_device`` (waits for it)."""

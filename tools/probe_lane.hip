@@ -37,7 +37,7 @@ struct Cols {
   uint32_t* sink;
 };
 
-enum : int { kU64 = 1, kStore = 2, kPipe = 4 };
+enum : int { kU64 = 1, kStore = 2, kPipe = 4, kCheck = 8 };
 
 template <int MODE>
 __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t nbytes, const uint64_t* st64,
@@ -67,6 +67,7 @@ __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t
       uint32_t p = __builtin_amdgcn_mov_dpp(e, 0x138, 0xf, 0xf, false);  // wave_shr:1
       if (lane == 0) p = r ? en32[r - 1] : 0u;
       s = p;
+      if ((MODE & kCheck) && s != (uint32_t)st64[r]) atomicAdd(c.sink + 1, 1u);
     }
   };
   auto window = [&](uint32_t e, uint32_t (&w)[16]) {
@@ -192,6 +193,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&c.blen, 4ull * n));
   CK(hipMalloc(&c.sink, 64));
   const int reps = 20;
+  CK(hipMemset(c.sink, 0, 64));
+  run<kCheck>(d_b, nb, d_s64, d_e64, d_e32, n, c, 2, 1);
+  uint32_t bad[2] = {0, 0};
+  CK(hipMemcpy(bad, c.sink, 8, hipMemcpyDeviceToHost));
+  printf("{\"dpp_wave_shr_check_mismatches\": %u}\n", bad[1]);
   printf("{\"records\": %u, \"bytes\": %u}\n", n, nb);
   auto rep = [&](const char* name, int mode, uint32_t tpw, float ms) {
     const double rd = (double)nb + (mode & kU64 ? 16.0 : 4.0) * n;
