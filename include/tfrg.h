@@ -218,8 +218,9 @@ typedef struct tfrg_info {
   uint32_t tpl_groups_missed; /* 64-record groups with a record no record-shape template took */
   uint32_t reserved;
   /* bit k: slot k (< 64) holds exactly one value per record, at row r of its column (final
-   * speculative placement). Its row splits are the identity 0..n and are NOT stored on the device
-   * (tfrg_result_device); tfrg_result_fetch writes them into the caller's buffer. */
+   * speculative placement). Its row splits are the identity 0..n: the decode does not store them;
+   * tfrg_result_fetch writes them into the caller's buffer, and tfrg_result_device into the device
+   * columns (one small kernel on the decode's stream, before it returns the view). */
   uint64_t placed_slots;
 } tfrg_info;
 
@@ -228,7 +229,6 @@ int tfrg_result_info(tfrg_ctx* ctx, tfrg_info* info);
 
 /* Columnar result. Per record: status/aux/verdict. Per slot s (row-major [n_slots][n]):
  * order (0 absent, else 1 + the key's position in the record's dict), row_splits [n_slots][n+1]
- * (device view: rows of tfrg_info.placed_slots are not stored, they are 0..n)
  * (element offsets inside the slot's column), slot_base [n_slots] (column start inside its kind's
  * value array). Values: int64, float bits, bytes views (absolute offset into the input buffer,
  * length). miss: [min(n_miss_entries, cap)][4] = (record, kind, key offset, key length). */
@@ -250,7 +250,9 @@ typedef struct tfrg_columns {
   uint64_t* bytes_offsets;
 } tfrg_columns;
 
-/* device pointers of the last result (valid until the next decode / destroy) */
+/* device pointers of the last result (valid until the next decode / destroy). Asynchronous: the
+ * columns are complete once the decode's stream reaches this call (it enqueues the identity row
+ * splits of the placed slots there, once per decode). */
 int tfrg_result_device(tfrg_ctx* ctx, tfrg_columns* cols);
 /* copy the last result into caller host buffers sized from tfrg_info; NULL members are skipped */
 int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);

@@ -75,3 +75,36 @@ def test_features_pickle_as_plain_features(batch):
         g = pickle.loads(pickle.dumps(f))
         assert type(g) is F.Feature
         assert g == f and g.fields == f.fields and g.fields_names == f.fields_names
+
+
+def test_gc_pause_is_refcounted_across_threads():
+    """hip._no_gc: overlapping builds on two threads re-enable the collector only when the last
+    one ends, and never when the caller had disabled it."""
+    import gc
+    import threading
+
+    from tfr_reader import hip
+
+    assert gc.isenabled()
+    inner, release = threading.Event(), threading.Event()
+
+    def other():
+        with hip._no_gc():
+            inner.set()
+            release.wait(5)
+
+    t = threading.Thread(target=other)
+    with hip._no_gc():
+        t.start()
+        inner.wait(5)
+    assert not gc.isenabled()  # the other thread's build is still running
+    release.set()
+    t.join()
+    assert gc.isenabled()
+    gc.disable()
+    try:
+        with hip._no_gc():
+            pass
+        assert not gc.isenabled()
+    finally:
+        gc.enable()

@@ -77,3 +77,24 @@ def test_public_api_cython_type():
                 e.features.feature["int64_feature"].float_list
     finally:
         set_decoder_type(old)
+
+
+def test_wide_record_is_linear_in_its_keys(orc):
+    """10^4 distinct keys (and each key again, last value wins, first position kept): the host
+    decoder interns keys through a hash table, so this takes milliseconds, not the seconds of a
+    linear scan per key; values and key order equal the oracle's."""
+    import time
+
+    from tests.golden.gen_golden import entry, example, i64
+
+    n = 10000
+    ents = [entry(b"k%05d" % i, i64(i)) for i in range(n)] + [entry(b"k%05d" % i, i64(-1)) for i in range(0, n, 7)]
+    payload = example(*ents)
+    t0 = time.perf_counter()
+    st, aux, got = host.decode_raw(payload)
+    dt = time.perf_counter() - t0
+    assert st == 0
+    ost, _, want = orc.decode(payload)
+    assert ost == 0 and got == want
+    assert len(got) == n and got[7][2] == [-1] and got[8][2] == [8]
+    assert dt < 0.2, dt

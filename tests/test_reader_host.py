@@ -109,3 +109,28 @@ def test_complex_bytes():  # test_reader.py:126-138
     raw = writer.encode_example([("image", "bytes_list", [img]), ("label", "int64_list", [7])])
     f = example.decode(raw)
     assert f["image"].value[0] == img and f["label"].value == [7]
+
+
+def test_threaded_random_access_over_more_files_than_kept_open(tmp_path):
+    """ds[i] from 8 threads over 12 files with at most 3 descriptors kept open: descriptors are
+    evicted while other threads read through them; every record still decodes to its own values."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    n_files, per = 12, 40
+    for f in range(n_files):
+        pl = [writer.encode_example([("f", "int64_list", [f]), ("i", "int64_list", [i])]) for i in range(per)]
+        writer.write_tfrecord(tmp_path / f"part-{f:02d}.tfrecord", pl, crc=True)
+    ds = tfr.load_from_directory(str(tmp_path))
+    ds.MAX_OPEN_FILES = 3
+    ds._files.cap = 3
+    want = {}
+    for j in range(ds.size):
+        feat = ds[j]
+        want[j] = (feat["f"].value[0], feat["i"].value[0])
+    order = np.random.default_rng(0).integers(0, ds.size, 4000).tolist()
+    with ThreadPoolExecutor(8) as ex:
+        got = list(ex.map(lambda j: (j, ds[j]["f"].value[0], ds[j]["i"].value[0]), order))
+    assert all(want[j] == (f, i) for j, f, i in got)
+    assert sorted(want.values()) == [(f, i) for f in range(n_files) for i in range(per)]
+    assert len(ds._files.items) <= 3
+    ds.close()

@@ -146,3 +146,38 @@ def test_large_records_and_strict_rejection():
     _same(pl, lane_max=0)
     _same(pl, lane_max=0, strict=True, corrupt=(5, 1500))
     _same([_reg(i) for i in range(3000)], strict=True, corrupt=(9, 2999))
+
+
+def test_device_view_row_splits_of_placed_slots():
+    """tfrg_result_device's columns are self-consistent: the row splits of the finally placed slots
+    (never stored by the decode) read 0..n from the device after a templated decode, like every
+    other row, on a context whose previous decode left other values in those rows."""
+    import ctypes
+
+    import torch
+
+    torch.zeros(1, device="cuda:0")
+    hip_rt = ctypes.CDLL("libamdhip64.so")
+    n = 6000
+    dec = hip.HipDecoder(0)
+    try:
+        pl = [_reg(i) for i in range(n)]
+        pl[5] = example(entry(b"label", i64(3, 4)), entry(b"id", byt(b"x")), entry(b"w", f32(1.0)), entry(b"k", i64(1)))
+        first = dec.decode(*synth.framed(pl))  # label irregular: its row splits are stored (scanned)
+        assert not (int(first.info.placed_slots) >> first.slot_key.index("label")) & 1
+        r = dec.decode(*synth.framed([_reg(i) for i in range(n)]))
+        placed = int(r.info.placed_slots)
+        assert placed
+        cols = dec.device_columns()
+        S = len(r.slot_key)
+        host = np.zeros((S, n + 1), np.uint32)
+        torch.cuda.synchronize()
+        rc = hip_rt.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(ctypes.cast(cols.row_splits, ctypes.c_void_p).value),
+                              ctypes.c_size_t(host.nbytes), 2)
+        assert rc == 0
+        for k in range(S):
+            assert np.array_equal(host[k], np.array(r.row_splits[k])), (k, (placed >> k) & 1)
+            if (placed >> k) & 1:
+                assert np.array_equal(host[k], np.arange(n + 1, dtype=np.uint32)), k
+    finally:
+        dec.close()

@@ -109,6 +109,7 @@ struct tfrg_ctx {
   uint64_t nbytes = 0;
   uint64_t cap_i64 = 0, cap_f32 = 0, cap_b = 0;
   bool have_result = false;
+  bool rs_complete = false;  // the placed slots' identity rows are written into the device columns
   // record-shape templates (tfrg_learn_templates): host key table, device templates
   std::unordered_map<std::string, uint32_t> key_id;
   std::vector<int32_t> key_slot_h;  // [4 * key]: flags, slot per kind
@@ -944,6 +945,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   c->last_stream = st;
   c->materialized = mat;
   c->have_result = true;
+  c->rs_complete = false;
   return 0;
 }
 
@@ -1019,6 +1021,15 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
 
 int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
   if (!c || !c->have_result) return TFRG_E_ARG;
+  if (!c->rs_complete && c->n_slots && c->n) {
+    // a self-consistent view: the identity rows of the finally placed slots, which the decode does
+    // not store, are written by one small kernel on the decode's stream (placed mask read on the
+    // device), once per decode
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_fill_placed_rows(c->rs.as<uint32_t>(), c->info.as<uint32_t>() + c->info_slot * kInfoCount,
+                                    c->n_slots, c->n, c->last_stream));
+  }
+  c->rs_complete = true;
   d->status = c->status.as<int32_t>();
   d->aux = c->aux.as<int64_t>();
   d->verdict = c->verdict.as<uint8_t>();

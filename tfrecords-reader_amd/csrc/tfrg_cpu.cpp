@@ -73,15 +73,37 @@ bool utf8_valid(const uint8_t* s, uint64_t n) {
 struct Ent {
   uint32_t koff, klen;
   int kind;
+  int kid;
   int64_t lo, ll;
 };
+
+// hash of a key's bytes (8 at a time)
+uint64_t key_hash(const uint8_t* s, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ n;
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, s + i, 8);
+    h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
+  }
+  uint64_t w = 0;
+  memcpy(&w, s + i, n - i);
+  h = (h ^ w) * 0x94D049BB133111EBull;
+  return h ^ (h >> 29);
+}
 
 }  // namespace
 
 struct tfrg_host_ctx {
-  // interned keys of the current call: (offset, length) into the payload, validity
+  // interned keys of the current call: (offset, length) into the payload, validity, hash; an
+  // open-addressing table over them (key id + 1, 0 = empty), so a record of K distinct keys costs
+  // O(K), as the reference's dict (decoder.pyx:141-150)
   std::vector<uint32_t> kof, kln;
   std::vector<uint8_t> kok;
+  std::vector<uint64_t> khash;
+  std::vector<uint32_t> kslot;  // key id -> its table slot
+  std::vector<int32_t> ht = std::vector<int32_t>(64, 0);
   std::vector<int32_t> pos_of;  // key id -> dict entry, -1 absent
   std::vector<Ent> ents;        // the dict, in insertion order
   const uint8_t* p = nullptr;
@@ -92,25 +114,47 @@ struct tfrg_host_ctx {
 
   // ---- the dict sink of tfrg_walk.h
   void reset() {
-    for (const Ent& e : ents) pos_of[intern_find(e.koff, e.klen)] = -1;
+    for (const Ent& e : ents) pos_of[e.kid] = -1;
     ents.clear();
   }
-  int intern_find(uint32_t off, uint32_t len) const {
-    for (size_t k = 0; k < kof.size(); ++k)
-      if (kln[k] == len && memcmp(p + kof[k], p + off, len) == 0) return (int)k;
-    return -1;
+  void clear_keys() {  // (only the used slots: a table grown by one wide record is not swept per call)
+    for (uint32_t sl : kslot) ht[sl] = 0;
+    kof.clear();
+    kln.clear();
+    kok.clear();
+    khash.clear();
+    kslot.clear();
+  }
+  void grow() {
+    const size_t m = ht.size() * 2;
+    ht.assign(m, 0);
+    for (size_t k = 0; k < kof.size(); ++k) {
+      size_t i = khash[k] & (m - 1);
+      while (ht[i]) i = (i + 1) & (m - 1);
+      ht[i] = (int32_t)k + 1;
+      kslot[k] = (uint32_t)i;
+    }
   }
   template <class S>
   int lookup(S&, int64_t off, int64_t len) {
     if (len > 0xffffffffll) return -2;
-    int k = intern_find((uint32_t)off, (uint32_t)len);
-    if (k < 0) {
-      k = (int)kof.size();
-      kof.push_back((uint32_t)off);
-      kln.push_back((uint32_t)len);
-      kok.push_back(utf8_valid(p + off, (uint64_t)len) ? 1 : 0);
-      pos_of.push_back(-1);
+    const uint32_t o = (uint32_t)off, n = (uint32_t)len;
+    const uint64_t h = key_hash(p + o, n);
+    const size_t m = ht.size() - 1;
+    size_t i = h & m;
+    for (; ht[i]; i = (i + 1) & m) {
+      const int k = ht[i] - 1;
+      if (khash[k] == h && kln[k] == n && memcmp(p + kof[k], p + o, n) == 0) return kok[k] ? k : -2;
     }
+    const int k = (int)kof.size();
+    kof.push_back(o);
+    kln.push_back(n);
+    kok.push_back(utf8_valid(p + o, (uint64_t)n) ? 1 : 0);
+    khash.push_back(h);
+    kslot.push_back((uint32_t)i);
+    ht[i] = k + 1;
+    pos_of.push_back(-1);
+    if (2 * kof.size() > ht.size()) grow();
     return kok[k] ? k : -2;
   }
   void note_miss(int, int64_t, int64_t) {}
@@ -122,7 +166,7 @@ struct tfrg_host_ctx {
       ents[at].ll = ll;
     } else {
       pos_of[kid] = (int)ents.size();
-      ents.push_back(Ent{(uint32_t)koff, (uint32_t)klen, kind_, lo, ll});
+      ents.push_back(Ent{(uint32_t)koff, (uint32_t)klen, kind_, kid, lo, ll});
     }
     return TFRG_OK;
   }
@@ -140,10 +184,8 @@ struct tfrg_host_ctx {
 
   template <bool COMPAT>
   int run(const uint8_t* payload, uint64_t len, int64_t& aux) {
+    clear_keys();
     p = payload;
-    kof.clear();
-    kln.clear();
-    kok.clear();
     pos_of.clear();
     ents.clear();
     key_off.clear();

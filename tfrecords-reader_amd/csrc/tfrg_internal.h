@@ -279,6 +279,7 @@ extern const char* const kStageNames[kNumStages];
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.
 hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* tpl, uint32_t w,
                            const uint32_t* d_tab, int num_cus, hipStream_t st);
+hipError_t launch_fill_placed_rows(uint32_t* rs, const uint32_t* info, uint32_t n_slots, uint32_t n, hipStream_t st);
 hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant);
 hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
                          const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream,

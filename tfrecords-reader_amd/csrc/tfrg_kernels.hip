@@ -3510,6 +3510,27 @@ hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o
   return launch_all<true>(b, sc, o, cfg, d_tab, d_consts, st, ev);
 }
 
+// Row splits of the finally placed slots (tfrg_info.placed_slots: the identity 0..n, never stored by
+// the decode) written into the device columns, for tfrg_result_device's view; the placed mask is
+// read from the decode's info words on the device (no host round trip).
+__global__ __launch_bounds__(256) void k_fill_placed_rows(uint32_t* __restrict__ rs, const uint32_t* __restrict__ info,
+                                                          uint32_t n_slots, uint32_t n) {
+  const uint64_t placed = ((uint64_t)info[kInfoPlacedHi] << 32) | info[kInfoPlacedLo];
+  const uint32_t k = blockIdx.y;
+  if (k >= 64u || k >= n_slots || !((placed >> k) & 1ull)) return;
+  uint32_t* row = rs + (size_t)k * (n + 1u);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i <= n; i += gridDim.x * 256u) row[i] = i;
+}
+
+hipError_t launch_fill_placed_rows(uint32_t* rs, const uint32_t* info, uint32_t n_slots, uint32_t n, hipStream_t st) {
+  const uint32_t slots = n_slots < 64u ? n_slots : 64u;
+  if (!slots) return hipSuccess;
+  const uint32_t blocks = (n + 1u + 255u) / 256u;
+  hipLaunchKernelGGL(k_fill_placed_rows, dim3(blocks < 1024u ? blocks : 1024u, slots), dim3(256), 0, st, rs, info,
+                     n_slots, n);
+  return hipGetLastError();
+}
+
 // Streaming read (measurement only): each block reads a contiguous slab, U 16-byte loads in flight
 // per lane (all issued before any is consumed), nontemporal (the data is not reused).
 typedef uint32_t sr_u32x4 __attribute__((ext_vector_type(4)));

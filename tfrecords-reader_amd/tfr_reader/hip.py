@@ -29,17 +29,30 @@ except ImportError:
 KIND_NAMES = {1: "bytes_list", 2: "float_list", 3: "int64_list"}
 
 
+_GC_LOCK = threading.Lock()
+_GC_DEPTH = 0       # batches being built right now, over all threads
+_GC_RESTORE = False  # the collector was enabled when the outermost of them began
+
+
 @contextlib.contextmanager
 def _no_gc():
     """Cyclic GC paused while a batch's Python objects are built: creating millions of lists and
-    tuples otherwise triggers generation scans over all of them (4-5x the construction time)."""
-    was = gc.isenabled()
-    gc.disable()
+    tuples otherwise triggers generation scans over all of them (4-5x the construction time).
+    Reference-counted over threads: the collector is re-enabled only when the last concurrent build
+    ends, and only if it was enabled when the first one began (a caller's own gc.disable() holds)."""
+    global _GC_DEPTH, _GC_RESTORE
+    with _GC_LOCK:
+        if _GC_DEPTH == 0:
+            _GC_RESTORE = gc.isenabled()
+            gc.disable()
+        _GC_DEPTH += 1
     try:
         yield
     finally:
-        if was:
-            gc.enable()
+        with _GC_LOCK:
+            _GC_DEPTH -= 1
+            if _GC_DEPTH == 0 and _GC_RESTORE:
+                gc.enable()
 
 #: records larger than this (framed bytes) are decoded one wavefront per record (libtfrg default)
 DEFAULT_LANE_MAX = 2048
@@ -220,6 +233,14 @@ class HipDecoder:
         info = N.TfrgInfo()
         N.check(self._lib.tfrg_result_info(self._ctx, C.byref(info)), "tfrg_result_info")
         return info
+
+    def device_columns(self) -> N.TfrgColumns:
+        """Device pointers of the last result (tfrg_result_device): valid until the next decode on
+        this decoder; the placed slots' identity row splits are written into them on the decode's
+        stream first."""
+        cols = N.TfrgColumns()
+        N.check(self._lib.tfrg_result_device(self._ctx, C.byref(cols)), "tfrg_result_device")
+        return cols
 
     def _learn_misses(self, buf: np.ndarray, info: N.TfrgInfo) -> bool:
         m = min(info.n_miss_entries, 1 << 16)

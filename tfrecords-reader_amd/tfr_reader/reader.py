@@ -13,6 +13,7 @@ import fnmatch
 import hashlib
 import os
 import struct
+import threading
 from collections.abc import Iterable, Sequence
 from pathlib import Path
 
@@ -276,6 +277,69 @@ def _load_files(dec, items, starts: np.ndarray, ends: np.ndarray, out: list, err
     flush()
 
 
+class _OpenSource:
+    __slots__ = ("kind", "value", "refs", "evicted")
+
+    def __init__(self, kind: str, value) -> None:
+        self.kind, self.value, self.refs, self.evicted = kind, value, 0, False
+
+
+def _open_record_source(path: str) -> _OpenSource:
+    _check_path(path)
+    if _io.is_compressed(path):
+        return _OpenSource("img", _io.file_image(path))
+    return _OpenSource("fd", os.open(path, os.O_RDONLY))
+
+
+class _OpenFiles:
+    """What ds[i] keeps open per file: a descriptor (plain files, one pread per record) or the
+    decompressed image (ZLIB / GZIP). Thread-safe: lookups, eviction of the oldest beyond ``cap``
+    and reference counts are under one lock, and an evicted descriptor is closed by its last reader,
+    so a pread never runs on a closed (or reused) descriptor. The reference opens the file per call
+    (reader.py:168-184) and shares nothing between threads."""
+
+    def __init__(self, cap: int) -> None:
+        self.cap = cap
+        self.lock = threading.Lock()
+        self.items: dict[str, _OpenSource] = {}
+
+    def acquire(self, path: str, opener=None):
+        with self.lock:
+            h = self.items.get(path)
+            if h is None:
+                if opener is None:
+                    return None
+                h = opener(path)
+                if len(self.items) >= self.cap:
+                    self._evict(self.items.pop(next(iter(self.items))))
+                self.items[path] = h
+            h.refs += 1
+            return h
+
+    def release(self, h: _OpenSource) -> None:
+        with self.lock:
+            h.refs -= 1
+            if h.evicted and h.refs == 0:
+                self._close(h)
+
+    def _evict(self, h: _OpenSource) -> None:
+        h.evicted = True
+        if h.refs == 0:
+            self._close(h)
+
+    @staticmethod
+    def _close(h: _OpenSource) -> None:
+        if h.kind == "fd" and h.value is not None:
+            os.close(h.value)
+        h.value = None
+
+    def close_all(self) -> None:
+        with self.lock:
+            items, self.items = self.items, {}
+            for h in items.values():
+                self._evict(h)
+
+
 class TFRecordDatasetReader:
     """Indexed TFRecord dataset (reader.py:79-290)."""
 
@@ -297,7 +361,7 @@ class TFRecordDatasetReader:
         self.index_df = F.with_row_index(index_df, "_row_id")
         self._sql = None
         self._cols = None  # (paths, file index per row, starts, ends), built on first access
-        self._files: dict = {}  # path -> ("fd", descriptor) | ("img", decompressed image), ds[i]
+        self._files = _OpenFiles(self.MAX_OPEN_FILES)  # ds[i]: descriptors / decompressed images
         self.logger.info(f"Loaded dataset index with N={F.height(self.index_df)} records ...")
 
     @property
@@ -349,12 +413,16 @@ class TFRecordDatasetReader:
                 raise IndexError(f"Index {idx=} out of bounds, dataset size={self.size}")
             start, end = int(st[idx]), int(en[idx])
             path = files[inv[idx]]
-            h = self._files.get(path)
-            if h is not None and h[0] == "fd" and end - start > 16 and end - start - 16 <= host.HOST_MAX_BYTES \
+            if end - start > 16 and end - start - 16 <= host.HOST_MAX_BYTES \
                     and example.feature.TFRECORD_READER_DECODER_IMP != "protobuf":
-                data = os.pread(h[1], end - start, start)
-                if len(data) == end - start:  # (else the general path below reports it)
-                    return host.decode(data[12:-4])
+                h = self._files.acquire(path)
+                if h is not None:
+                    try:
+                        data = os.pread(h.value, end - start, start) if h.kind == "fd" else None
+                    finally:
+                        self._files.release(h)
+                    if data is not None and len(data) == end - start:  # (else the general path reports it)
+                        return host.decode(data[12:-4])
         if isinstance(idx, Iterable):
             idxs = [int(i) for i in idx]
             for i in idxs:
@@ -382,26 +450,18 @@ class TFRecordDatasetReader:
         """Bytes [start, end) of one file (reader.py:36-56 reads them with seek + read per call): a
         plain file is read with one pread on a descriptor kept open by this dataset, a ZLIB / GZIP
         file is sliced from its decompressed image (tfr_reader/_io.py)."""
-        h = self._files.get(path)
-        if h is None:
-            _check_path(path)
-            h = ("img", _io.file_image(path)) if _io.is_compressed(path) else ("fd", os.open(path, os.O_RDONLY))
-            if len(self._files) >= self.MAX_OPEN_FILES:
-                old = self._files.pop(next(iter(self._files)))
-                if old[0] == "fd":
-                    os.close(old[1])
-            self._files[path] = h
-        if h[0] == "fd":
-            return os.pread(h[1], max(end - start, 0), start) if end > start else b""
-        img = h[1]
-        return img[start:end].tobytes() if start < img.size else b""
+        h = self._files.acquire(path, opener=_open_record_source)
+        try:
+            if h.kind == "fd":
+                return os.pread(h.value, max(end - start, 0), start) if end > start else b""
+            img = h.value
+            return img[start:end].tobytes() if start < img.size else b""
+        finally:
+            self._files.release(h)
 
     def close(self) -> None:
-        """Close the file descriptors ds[i] keeps open."""
-        for kind, v in self._files.values():
-            if kind == "fd":
-                os.close(v)
-        self._files = {}
+        """Close the file descriptors ds[i] keeps open (one still being read is closed by its reader)."""
+        self._files.close_all()
 
     def __del__(self):  # noqa: D105
         try:
