@@ -51,7 +51,9 @@ enum tfrg_status {
   TFRG_UB_READ_PAST_END = 35,   /* decode_varint (decoder.pyx:34-50) past the NUL terminator */
   /* build-internal (never surfaced as a decode result) */
   TFRG_ST_SCHEMA_MISS = 64,     /* a key/kind not in the device key table: intern and re-run  */
-  TFRG_ST_LIMIT = 65            /* a build limit (e.g. > 65534 keys in one record)            */
+  TFRG_ST_LIMIT = 65,           /* a build limit (e.g. > 65534 keys in one record)            */
+  TFRG_ST_INTERNAL = 66         /* a device-internal list location outside its record (a stale or
+                                   corrupt count / loc word): the list is not walked; aux = slot */
 };
 
 /* Feature kinds, numbered as the tf.train.Feature oneof field numbers (decoder.pyx:179-197). */

@@ -42,7 +42,7 @@ def test_status_messages_match_the_python_mirror():
 
     lib = N.lib()
     codes = [c for c in range(0, 70) if c in S.MESSAGES or c in S.UB_CODES or c in (
-        S.ERR_WIRE_TYPE, S.ERR_FEATURES_NONE, S.ERR_READ, S.ERR_CRC, S.ST_LIMIT)]
+        S.ERR_WIRE_TYPE, S.ERR_FEATURES_NONE, S.ERR_READ, S.ERR_CRC, S.ST_LIMIT, S.ST_INTERNAL)]
     assert len(codes) >= 19
     for code in codes:
         for aux in (0, 3, 7):

@@ -129,6 +129,8 @@ struct tfrg_ctx {
   bool profiling = false;
   bool have_events = false;
   hipEvent_t ev[kNumStages + 1] = {};
+  // debug hook: records whose list locations are poisoned after the count passes (tests)
+  uint32_t poison[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 };
 
 extern "C" {
@@ -146,6 +148,13 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
+  if (const char* e = getenv("TFRG_DEBUG_POISON_LOC")) {  // "r0,r1,..." (at most 4)
+    char* q = const_cast<char*>(e);
+    for (int i = 0; i < 4 && *q; ++i) {
+      c->poison[i] = (uint32_t)strtoul(q, &q, 10);
+      while (*q == ',' || *q == ' ') ++q;
+    }
+  }
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess) c->num_cus = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
@@ -877,6 +886,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   cfg.wave_grid = (int)(wave_blocks < 1 ? 1 : (wave_blocks < wave_cap ? wave_blocks : wave_cap));
   cfg.lane_max = c->lane_max;
   cfg.wave_stage = c->wave_stage;
+  memcpy(cfg.poison, c->poison, sizeof(cfg.poison));
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
   // deferred packed bodies when records above lane_max may be walked from HBM: one 64-row block

@@ -81,7 +81,7 @@ const char* tfrg_status_exception(int status) {
     case TFRG_ERR_CRC: return "DataLossError";             // TFRG_FLAG_STRICT_CRC (OSError subclass)
     case TFRG_UB_EMPTY_FEATURE: case TFRG_UB_SHORT_MAP_ENTRY: case TFRG_UB_NEGATIVE_LENGTH:
     case TFRG_UB_READ_PAST_END: return "UndefinedRecordError";
-    case TFRG_ST_SCHEMA_MISS: case TFRG_ST_LIMIT: return "RuntimeError";
+    case TFRG_ST_SCHEMA_MISS: case TFRG_ST_LIMIT: case TFRG_ST_INTERNAL: return "RuntimeError";
     default: return status >= TFRG_ERR_VARINT_TOO_MANY && status <= TFRG_ERR_WT_INT64_LIST ? "Exception"
                                                                                              : "RuntimeError";
   }
@@ -132,6 +132,10 @@ const char* tfrg_status_message(int status, int64_t aux) {
       m = "varint runs past the end of the record (undefined in the reference: decoder.pyx:34-50 has no bound)";
       break;
     case TFRG_ST_LIMIT: m = "record exceeds a decoder limit (more than 65534 keys)"; break;
+    case TFRG_ST_INTERNAL:
+      snprintf(buf, sizeof(buf), "internal decoder error: list location of slot %lld outside its record",
+               (long long)aux);
+      return buf;
     default:
       snprintf(buf, sizeof(buf), "unexpected decoder status %d", status);
       return buf;

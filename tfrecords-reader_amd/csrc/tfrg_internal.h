@@ -269,6 +269,8 @@ struct LaunchCfg {
   uint32_t lane_max;       // records above this size go to the wave kernels
   uint32_t wave_stage;     // wave records spanning <= this many bytes are staged in LDS (<= kWStage)
   bool body_count;         // deferred packed bodies possible (DevOut::dq): launch k_body_count
+  uint32_t poison[4];      // debug hook (env TFRG_DEBUG_POISON_LOC): records whose list locations are
+                           // overwritten after the count passes (0xffffffff: none)
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).

@@ -2593,6 +2593,26 @@ struct ColOut {
     ++dst;
   }
 };
+// A list location must lie inside its record's payload: every location the count passes write does
+// (lo + len <= L). A word that does not -- stale or corrupt -- would send a gather walk through bytes
+// outside the record (and, with a garbage length, on for billions of steps), so the record fails
+// with TFRG_ST_INTERNAL (aux = the slot) and the list is not walked.
+__device__ __forceinline__ bool loc_in_record(uint2 lc, int64_t L) {
+  return (uint64_t)lc.x + lc.y <= (uint64_t)(L < 0 ? 0 : L);
+}
+__device__ void loc_fail(const DevOut& o, uint32_t r, uint32_t k, uint2 lc) {
+  if (atomicExch(&o.status[r], (int)TFRG_ST_INTERNAL) == TFRG_OK) {
+    o.aux[r] = k;
+    atomicAdd(&o.info[kInfoErrors], 1u);
+    atomicMax(&o.info[kInfoFirstError], ~r);
+  }
+#if defined(TFRG_DEBUG)
+  printf("tfrg: record %u slot %u: list location (%u, %u) outside its record\n", r, k, lc.x, lc.y);
+#else
+  (void)lc;
+#endif
+}
+
 template <bool COMPAT, class S>
 __device__ void list_gather(S& s, const DevOut& o, int kind, int64_t lo, int64_t ll, uint64_t dst) {
   ColOut out{o, s.p0, dst};
@@ -2656,6 +2676,10 @@ __device__ __forceinline__ void gather_record(const DevBatch& B, const DevSchema
     const uint32_t c = o.count[at];
     if (!c || (c & kCountInline)) continue;
     const uint2 lc = o.loc[at];
+    if (!loc_in_record(lc, s.L)) {
+      loc_fail(o, r, k, lc);
+      continue;
+    }
     const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
     list_gather<COMPAT>(s, o, sc.slot_kind[k], (int64_t)lc.x, (int64_t)lc.y, dst);
   }
@@ -2828,6 +2852,10 @@ __device__ void role_list_gather(const DevBatch& B, const DevSchema& sc, const D
           const uint32_t c = o.count[at];
           if (!c || (c & kCountInline)) continue;
           const uint2 lc = o.loc[at];
+          if (!loc_in_record(lc, v.L)) {
+            loc_fail(o, r, k, lc);
+            continue;
+          }
           const uint32_t kind = sc.slot_kind[k];
           const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
           if (!fast_list_gather<COMPAT>(fs, o, kind, lc.x, lc.y, dst))
@@ -2858,6 +2886,10 @@ __device__ void role_wave_gather(const DevBatch& B, const DevSchema& sc, const D
       const uint32_t c = o.count[at];
       if (!c || (c & kCountInline)) continue;  // absent / empty, or written inline by k_down_gather
       const uint2 lc = o.loc[at];
+      if (!loc_in_record(lc, v.L)) {
+        loc_fail(o, r, k, lc);
+        continue;
+      }
       const uint64_t dst = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
       Src s;
       s.init(B.bytes, v.p0, v.L);
@@ -3288,7 +3320,7 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     const uint32_t c = c_n, kind = kind_l;
     const uint2 lc = lc_n;
     const uint64_t dst = sbase_l + rs_n;
-    const bool present = c && !(c & kCountInline);  // inline single values are k_down_gather's
+    bool present = c && !(c & kCountInline);  // inline single values are k_down_gather's
     q.r1 = q.r2;
     q.s1 = rfl64(q.s2v);
     q.e1 = rfl64(q.e2v);
@@ -3303,6 +3335,10 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
     if (!ok) continue;  // wave-uniform
     PHASE_MARK(t1);
     PHASE_ADD(9, t0, t1);
+    if (present && !loc_in_record(lc, v.L)) {  // (lane = slot)
+      loc_fail(o, r, lane, lc);
+      present = false;
+    }
     const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
     stage_gather_group<COMPAT>(fs, o, present, kind, lc, c, dst, lo16, lane, ring);
     for (uint32_t kb = 64; kb < sc.n_slots; kb += 64) {  // wide schemas: further groups of 64 slots
@@ -3318,6 +3354,10 @@ __device__ void role_stage_gather(const DevBatch& B, const DevSchema& sc, const 
         lk = o.loc[at];
         dk = o.slot_base[k] + o.rs[(size_t)k * (B.n + 1) + r];
         kk = sc.slot_kind[k];
+        if (pk && !loc_in_record(lk, v.L)) {
+          loc_fail(o, r, k, lk);
+          pk = false;
+        }
       }
       stage_gather_group<COMPAT>(fs, o, pk, kk, lk, ck, dk, lo16, lane, ring);
     }
@@ -3343,6 +3383,16 @@ __global__ __launch_bounds__(kWaveBlock) void k_tail_gather(DevBatch B, DevSchem
   role_list_gather<COMPAT>(B, sc, o, lane_max, stage, placed);
   role_stage_gather<COMPAT>(B, sc, o, stage, ring, placed);
   role_wave_gather<COMPAT>(B, sc, o, placed);
+}
+
+// Debug hook (tfrg_ctx: env TFRG_DEBUG_POISON_LOC at context creation): after the count passes,
+// the list locations of up to 4 records are overwritten with a location far outside any record, as
+// a stale or corrupt word would be; the gathers must then fail those records (TFRG_ST_INTERNAL).
+__global__ void k_poison_loc(DevOut o, uint32_t n, uint32_t n_slots, uint4 recs) {
+  const uint32_t rr[4] = {recs.x, recs.y, recs.z, recs.w};
+  for (uint32_t k = threadIdx.x; k < n_slots; k += blockDim.x)
+    for (int i = 0; i < 4; ++i)
+      if (rr[i] < n) o.loc[(size_t)k * n + rr[i]] = make_uint2(0xfffff000u, 0x00ffffffu);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -3469,6 +3519,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab,
                          d_consts, cfg.lane_max);
   }
+  if (cfg.poison[0] != 0xffffffffu && S > 0)
+    hipLaunchKernelGGL(k_poison_loc, dim3(1), dim3(64), 0, st, ox, b.n, (uint32_t)S,
+                       make_uint4(cfg.poison[0], cfg.poison[1], cfg.poison[2], cfg.poison[3]));
   mark(kStageSpine);
   if (S > 0)
     hipLaunchKernelGGL(k_spine, dim3(o.n_chunks * (uint32_t)S), dim3(kSpineBlock), 0, st, ox, sc.slot_kind, (uint32_t)S, n_tiles,

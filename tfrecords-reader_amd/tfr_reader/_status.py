@@ -30,6 +30,7 @@ UB_NEGATIVE_LENGTH = 34
 UB_READ_PAST_END = 35
 ST_SCHEMA_MISS = 64
 ST_LIMIT = 65
+ST_INTERNAL = 66
 
 UB_CODES = frozenset({UB_EMPTY_FEATURE, UB_SHORT_MAP_ENTRY, UB_NEGATIVE_LENGTH, UB_READ_PAST_END})
 
@@ -93,6 +94,8 @@ def exception_for(status: int, aux: int, payload_key: bytes | None = None) -> Ba
         return UndefinedRecordError(UB_MESSAGES[status])
     if status == ST_LIMIT:
         return RuntimeError("record exceeds a decoder limit (more than 65534 keys)")
+    if status == ST_INTERNAL:
+        return RuntimeError(f"internal decoder error: list location of slot {aux} outside its record")
     return RuntimeError(f"unexpected decoder status {status}")
 
 
