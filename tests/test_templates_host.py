@@ -53,7 +53,7 @@ def _learn(keys, slots, buf, st, en):
     offs[1:] = np.cumsum([len(k) for k in keys])
     sk = np.array([s[0] for s in slots], np.uint32)
     sd = np.array([s[1] for s in slots], np.uint8)
-    out = np.zeros(4 * K_WORDS, np.uint32)
+    out = np.zeros(32 * K_WORDS, np.uint32)
     W = np.zeros(1, np.uint32)
     b = np.frombuffer(blob, np.uint8)
     nt = N.lib().tfrg_learn_templates_host(len(keys), N.ptr(b), N.ptr(offs), None, len(slots), N.ptr(sk), N.ptr(sd),

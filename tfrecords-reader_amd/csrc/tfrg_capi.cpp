@@ -116,6 +116,8 @@ struct tfrg_ctx {
   DBuf tpl;
   uint32_t n_tpl = 0;
   uint32_t tpl_w = 0;  // window words of the templates (16 / 32 / 64)
+  size_t tpl_img_off = 0;  // the lane image follows the window-form templates in tpl
+  uint32_t tpl_img_words = 0;
   std::vector<uint32_t> tpl_h;  // host copy of the template words
   bool tpl_learned = false;
   bool tpl_on = true;
@@ -368,6 +370,8 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   s.key_w = c->key_w.as<uint32_t>();
   s.krec = c->krec.as<uint32_t>();
   s.tpl = c->tpl.as<uint32_t>();
+  s.tpl_img = s.tpl + c->tpl_img_off;
+  s.tpl_img_words = c->tpl_img_words;
   s.n_tpl = c->tpl_on ? c->n_tpl : 0u;
   s.tpl_w = c->tpl_w;
   // speculative placement is a property of the learned shapes' schema (a slot that is one inline
@@ -500,7 +504,7 @@ bool tpl_derive(const TplSchema* c, const uint8_t* p, uint32_t L, Tpl& t) {
 // Record shapes of a host sample -> window-form templates (tfrg_internal.h) + the speculative
 // placement words. Returns the template count (0: none).
 struct Learned {
-  std::vector<uint32_t> w, spec;
+  std::vector<uint32_t> w, spec, img;  // window-form templates, spec words, lane image
   uint32_t W = 0;
   bool have_spec = false;
 };
@@ -508,8 +512,11 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
                       const uint64_t* h_end, uint32_t n, uint32_t flags, Learned& out) {
   std::map<std::string, std::pair<uint32_t, Tpl>> seen;  // shape -> (records, template)
   Tpl t;
+  // up to 4,096 records spread over the whole batch (not its first ones: ids that grow with the
+  // record index give the first records shapes the rest of a file does not have)
   const uint32_t lim = n < 4096u ? n : 4096u;
-  for (uint32_t i = 0; i < lim; ++i) {
+  for (uint32_t j = 0; j < lim; ++j) {
+    const uint32_t i = (uint32_t)((uint64_t)j * n / lim);
     uint64_t a = h_start[i], e = h_end[i];
     if (e > nbytes || e < a) continue;
     if (!(flags & TFRG_FLAG_PAYLOAD_ONLY)) {  // framed: a length field matching the range
@@ -526,9 +533,13 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
     ++slot.first;
   }
   std::vector<std::pair<uint32_t, const Tpl*>> order;
-  for (auto& kv : seen) order.push_back({kv.second.first, &kv.second.second});
+  // shapes seen at least twice in a large sample (a one-off shape would only cost the kernel a
+  // template and could turn a speculatively placed slot irregular), the most frequent first
+  const uint32_t min_count = lim >= 256u ? 2u : 1u;
+  for (auto& kv : seen)
+    if (kv.second.first >= min_count) order.push_back({kv.second.first, &kv.second.second});
   std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-  const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMax);
+  const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMaxLane);
   if (!nt) return 0;
   // speculative placement (DevSchema::spec): slots that are an inline single value in every kept
   // template, taken per kind in slot order up to the first slot of that kind that is not one (its
@@ -625,8 +636,54 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
     }
     d[kLtAbsent] = ~present & (S >= kLeanMaxSlots ? 0xffffu : ((1u << S) - 1u));
   }
+  // the lane image (tfrg_internal.h kLi*): per-lane template words, the length table, per-slot ranges
+  const uint32_t tw = kLiTw(W);
+  std::vector<uint32_t> img(kLiTpl + (size_t)nt * tw, 0);
+  img[0] = nt;
+  img[1] = W;
+  img[2] = tw;
+  img[4] = W;
+  std::vector<uint8_t> lut(kTplMaxL + 1, 0xffu);
+  for (uint32_t k = 0; k < nt; ++k) {
+    const uint32_t* d = &w[(size_t)k * kLtWords];
+    uint32_t* q = &img[kLiTpl + (size_t)k * tw];
+    const uint32_t L = d[kLtL];
+    q[0] = L;
+    q[1] = d[kLtK];
+    q[2] = 0xffu;
+    for (uint32_t i = 0; i < 3 * W; ++i) q[4 + i] = d[kLtWin + (i / W) * W + i % W];
+    for (uint32_t s2 = 0; s2 < kLeanMaxSlots; ++s2) {
+      const uint32_t* z = d + kLtSlot + 3 * s2;
+      uint32_t* y = q + 4 + 3 * W + 4 * s2;
+      y[0] = z[0];
+      y[1] = z[1];
+      y[2] = z[2];
+      const uint32_t mode = z[0] & 0xffu, rk = z[0] >> 16;
+      uint32_t& sq = img[kLiSlotQ + s2];
+      if (rk && (mode == 1u || mode == 2u)) {  // an inline value in window words [pos / 4, pos / 4 + 1]
+        const uint32_t qw = z[1] >> 2;
+        const uint32_t lo = (sq & kLiQValue) ? std::min(sq & 0xffu, qw) : qw;
+        const uint32_t hi = (sq & kLiQValue) ? std::max((sq >> 8) & 0xffu, qw) : qw;
+        sq = (sq & kLiQSingle) | kLiQValue | lo | (hi << 8);
+      }
+      if (k == 0) sq |= kLiQSingle;
+      if ((z[2] & ~kCountInline) > 1u) sq &= ~kLiQSingle;
+    }
+    img[3] |= d[kLtCrcw];
+    img[4] = std::min(img[4], d[kLtChain]);
+    // the length chain: templates of one length in order of frequency
+    if (lut[L] == 0xffu) {
+      lut[L] = (uint8_t)k;
+    } else {
+      uint32_t p = lut[L];
+      while (img[kLiTpl + (size_t)p * tw + 2] != 0xffu) p = img[kLiTpl + (size_t)p * tw + 2];
+      img[kLiTpl + (size_t)p * tw + 2] = k;
+    }
+  }
+  memcpy(&img[kLiLut], lut.data(), lut.size());
   out.w = std::move(w);
   out.spec = std::move(spec);
+  out.img = std::move(img);
   out.W = W;
   out.have_spec = have_spec;
   return nt;
@@ -652,11 +709,14 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   const uint32_t W = L.W;
   HIP_TRY(hipSetDevice(c->device));
   if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
-  if (c->tpl.ensure(w.size() * 4) || (have_spec && c->spec.ensure((size_t)S * 4))) {
+  if (c->tpl.ensure((w.size() + L.img.size()) * 4) || (have_spec && c->spec.ensure((size_t)S * 4))) {
     set_error("template allocation failed");
     return TFRG_E_NOMEM;
   }
   HIP_TRY(hipMemcpy(c->tpl.p, w.data(), w.size() * 4, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->tpl.as<uint32_t>() + w.size(), L.img.data(), L.img.size() * 4, hipMemcpyHostToDevice));
+  c->tpl_img_off = w.size();
+  c->tpl_img_words = (uint32_t)L.img.size();
   if (have_spec) HIP_TRY(hipMemcpy(c->spec.p, spec.data(), (size_t)S * 4, hipMemcpyHostToDevice));
   c->n_tpl = nt;
   c->tpl_w = W;

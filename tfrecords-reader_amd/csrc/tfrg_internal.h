@@ -21,6 +21,8 @@ struct DevSchema {
   const uint32_t* key_w;       // [n_keys][2]: first / last 4 key bytes (see key_hash_words)
   const uint32_t* krec;        // [n_keys][8] packed key record, see KeyRec
   const uint32_t* tpl;         // [n_tpl][kLtWords] record-shape templates in window form (below)
+  const uint32_t* tpl_img;     // their lane image (kLiHdr ...), tpl_img_words words
+  uint32_t tpl_img_words;
   uint32_t n_tpl;
   uint32_t tpl_w;              // their window words W (16, 32 or 64)
   // [n_slots] speculative placement of single values (null = off): 0, or (rank + 1) << 2 | kind for
@@ -61,6 +63,27 @@ constexpr uint32_t kLtL = 0, kLtNe = 1, kLtCrcw = 2, kLtChain = 3, kLtK = 4, kLt
                    kLtWords = kLtSlot + 3 * kLeanMaxSlots;
 constexpr uint32_t kLeanTabOff = 51200;  // crc_tab words: T_d, d < 32, 256 entries each (slice-by-32)
 
+// Lane image of the templates (k_tpl_lane): each lane matches the template its record's payload
+// length selects, so the template words are read per lane from LDS, where the workgroup copies this
+// image. Built on the host from the window-form templates (tfrg_learn_templates) and stored after
+// them in the template buffer (DevSchema::tpl_img). u32 words:
+//   header [0, kLiHdr): [0] templates, [1] W, [2] words per template (kLiTw), [3] union over the
+//     templates of kLtCrcw, [4] the smallest kLtChain;
+//   [kLiSlotQ + k] slot k (< kLeanMaxSlots): qlo | qhi << 8 | kLiQValue (some template holds an
+//     inline int64 / float there, in window words qlo .. qhi + 1) | kLiQSingle (no template has more
+//     than one value there);
+//   [kLiLut, + kLiLutWords) bytes: for payload length L <= kTplMaxL the first template of that
+//     length (0xff: none);
+//   [kLiTpl + t kLiTw(W)] template t: [0] L, [1] K, [2] the next template of the same length
+//     (0xff: none), [4, 4 + W) Bm, [4 + W, 4 + 2 W) Mm, [4 + 2 W, 4 + 3 W) Cm, then per slot k 4 words
+//     {mode | len << 8 | rank << 16 (0: absent), pos, count word (0: absent), 0}
+//     (tfrg_internal.h "Record-shape template" for the fields).
+constexpr uint32_t kTplMaxLane = 32;  // templates kept for the lane kernel (the most frequent shapes)
+constexpr uint32_t kLiHdr = 8, kLiSlotQ = kLiHdr, kLiLut = kLiSlotQ + kLeanMaxSlots,
+                   kLiLutWords = (kTplMaxL + 1 + 3) / 4, kLiTpl = (kLiLut + kLiLutWords + 3) & ~3u;
+constexpr uint32_t kLiQValue = 1u << 16, kLiQSingle = 1u << 17;
+__host__ __device__ constexpr uint32_t kLiTw(uint32_t W) { return 4 + 3 * W + 4 * kLeanMaxSlots; }
+
 // Column targets of one slot for k_tpl_lane, computed on the host per decode.
 struct LeanTgt {
   uint16_t* ord;   // order column of the slot
@@ -79,6 +102,7 @@ struct LeanArgs {
   uint32_t* tsum;  // tile sums, slot k's at k * tile_stride
   uint32_t n_slots;
   uint32_t tile_stride;
+  uint32_t img_words;  // the templates' lane image (DevSchema::tpl_img), copied into LDS
   uint32_t gpw;    // (launch_tpl_lane) 64-record groups per wave: 2 (half a tile: small batches,
                    // twice the waves, tile sums added atomically) or a multiple of 4 (whole tiles)
   LeanTgt tg[kLeanMaxSlots];
@@ -279,7 +303,7 @@ enum Stage : int { kStageTplLane = 0, kStageLaneCount, kStageBodyCount, kStageTa
 extern const char* const kStageNames[kNumStages];
 
 // ev: optional kNumStages + 1 events recorded on `stream` before each stage and after the last.
-hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* tpl, uint32_t w,
+hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* img, uint32_t w,
                            const uint32_t* d_tab, int num_cus, hipStream_t st);
 hipError_t launch_fill_placed_rows(uint32_t* rs, const uint32_t* info, uint32_t n_slots, uint32_t n, hipStream_t st);
 hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant);

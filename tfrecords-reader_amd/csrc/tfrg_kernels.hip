@@ -3441,6 +3441,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   if (lean) {
     LeanArgs a{};
     a.n_tpl = sc.n_tpl;
+    a.img_words = sc.tpl_img_words;
     a.lane_max = cfg.lane_max;
     a.tsum = o.tsum;
     a.n_slots = (uint32_t)S;
@@ -3465,7 +3466,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
         t.v2 = o.b_len + base;
       }
     }
-    const hipError_t e = launch_tpl_lane(b, ox, a, sc.tpl, sc.tpl_w, d_tab, cfg.num_cus, st);
+    const hipError_t e = launch_tpl_lane(b, ox, a, sc.tpl_img, sc.tpl_w, d_tab, cfg.num_cus, st);
     if (e != hipSuccess) return e;
   }
   mark(kStageLaneCount);

@@ -34,6 +34,9 @@ namespace {
 constexpr int kTplBlock = 512;        // 8 waves: the 32 KiB of tables are shared by 8 waves
 constexpr uint32_t kTplTabs = 32;     // T_0 .. T_31
 constexpr uint32_t kHitVerdict = TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC;
+#ifndef TFRG_TPL_GROUPS_PER_STEP
+#define TFRG_TPL_GROUPS_PER_STEP 1
+#endif
 
 typedef __attribute__((address_space(4))) const uint32_t cu32;  // wave-uniform reads -> s_load
 
@@ -91,16 +94,28 @@ struct LaneOff {
   uint32_t s, e;
 };
 
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+#pragma unroll
+  for (int m = 1; m < 64; m <<= 1) x += (uint32_t)__shfl_xor((int)x, m, 64);
+  return x;
+}
+
 template <int W, int OM>
 __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_tpl_lane(
-    DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ tpl, const uint32_t* __restrict__ tabs) {
+    DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ img, const uint32_t* __restrict__ tabs) {
   static_assert(W == 16 || W == 32 || W == 64, "window words");
   typedef uint32_t wvec __attribute__((ext_vector_type(W)));
   __shared__ uint32_t tab[kTplTabs * 256];
+  extern __shared__ __attribute__((aligned(16))) uint32_t limg[];  // the templates' lane image
   for (uint32_t i = threadIdx.x; i < kTplTabs * 256; i += kTplBlock) tab[i] = tabs[i];
+  for (uint32_t i = threadIdx.x; i < A.img_words; i += kTplBlock) limg[i] = img[i];
   __syncthreads();
   constexpr uint32_t kWaves = kTplBlock / 64;
+  constexpr uint32_t kTw = kLiTw(W);
   const uint32_t lane = threadIdx.x & 63u, wib = rfl(threadIdx.x >> 6);
+  cu32* gimg = (cu32*)img;  // (the image's wave-uniform words: scalar loads)
+  const uint32_t crcw_u = gimg[3], chain_u = gimg[4];
+  const uint8_t* lut = reinterpret_cast<const uint8_t*>(limg + kLiLut);
   // batches are < 0xffffff00 bytes (launch_tpl_lane): an offset of 0xffffff00 reads zeros
   const __amdgpu_buffer_rsrc_t rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(B.bytes), (short)0, (int)(uint32_t)B.nbytes, 0x00020000);
@@ -184,84 +199,85 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
   };
   uint32_t acc = 0;  // lane k: slot k's value count over this tile's records so far
-  // one group: template match + CRC (-> tsel, the lane's template), then the dict into the columns
+  // one group: every lane matches the template its payload length selects (kLiLut; the next one of
+  // the same length if that fails), then the dict into the columns, one store per column
   auto proc = [&](const wvec& w, uint32_t g, const LaneOff& f) {
     const uint32_t r = (g << 6) + lane;
     const bool valid = r < B.n;
     const uint32_t st = start_of(f), en = f.e;
     const bool inb = in_batch(g, st, en);
     const uint32_t rl = en - st;
-    uint32_t tsel = kTplMax;  // (none)
-    uint32_t hmask = 0;       // templates with hits (wave-uniform)
-    uint32_t hcnt = 0;        // their hit counts, 8 bits each (wave-uniform)
-    for (uint32_t t = 0; t < A.n_tpl; ++t) {  // (wave-uniform)
-      cu32* tp = (cu32*)tpl + t * kLtWords;
-      const uint32_t L = tp[kLtL];
-      if (L + 16u > A.lane_max) continue;  // (its records belong to the wavefront kernels)
-      const bool cand = inb && tsel == kTplMax && rl == L + 16u;
-      if (!__ballot(cand)) continue;
+    // (records above lane_max belong to the wavefront kernels)
+    uint32_t cand = inb && rl >= 16u && rl - 16u <= kTplMaxL && rl <= A.lane_max ? (uint32_t)lut[rl - 16u] : 0xffu;
+    uint32_t tsel = 0xffu;
+    while (__ballot(cand != 0xffu)) {  // (usually one pass: lengths rarely share templates)
+      const bool act = cand != 0xffu;
+      const uint32_t* tp = limg + kLiTpl + (act ? cand : 0u) * kTw;
+      const u32x4 meta = *reinterpret_cast<const u32x4*>(tp);  // L, K, next
       uint32_t diff = 0;
 #pragma unroll
-      for (int i = 0; i < W - 1; ++i) diff |= (w[i] ^ tp[kLtWin + i]) & tp[kLtWin + W + i];
-      // payload CRC-32C: variable bits further than 32 bytes from the end through a slice-by-4
-      // chain (its state joins word W - 9, distances 28..31), the last 32 bytes by position tables
+      for (int q = 0; q < W / 4; ++q) {
+        const u32x4 bm = *reinterpret_cast<const u32x4*>(tp + 4 + 4 * q);
+        const u32x4 mm = *reinterpret_cast<const u32x4*>(tp + 4 + W + 4 * q);
+        diff |= ((w[4 * q] ^ bm.x) & mm.x) | ((w[4 * q + 1] ^ bm.y) & mm.y) | ((w[4 * q + 2] ^ bm.z) & mm.z) |
+                ((w[4 * q + 3] ^ bm.w) & mm.w);
+        // (one quarter of the template's words live at a time: hoisting all of them costs 32 VGPRs,
+        // i.e. occupancy; other waves cover the LDS latency)
+        if (q & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+      // payload CRC-32C over the words where any template has variable bits (this lane's template
+      // masks them, Cm): variable bits further than 32 bytes from the end through a slice-by-4 chain
+      // (its state joins word W - 9, distances 28..31), the last 32 bytes by position tables
+      const uint32_t* cm = tp + 4 + 2 * W;
       uint32_t c = 0;
-      const uint32_t chain = tp[kLtChain];
-      if (chain < (uint32_t)(W - 9)) {
+      if (chain_u < (uint32_t)(W - 9)) {
 #pragma unroll
         for (int i = 0; i < W - 9; ++i)
-          if ((uint32_t)i >= chain) c = lin_word<0>(tab, c ^ (w[i] & tp[kLtWin + 2 * W + i]));
+          if ((uint32_t)i >= chain_u) c = lin_word<0>(tab, c ^ (w[i] & cm[i]));
       }
-      const uint32_t crcw = tp[kLtCrcw];
       uint32_t lin = 0;
-#define TFRG_LIN(j)                                                                              \
-  if (crcw & (1u << (j))) lin ^= lin_word<28 - 4 * (j)>(tab, (w[W - 9 + (j)] & tp[kLtWin + 2 * W + W - 9 + (j)]) ^ \
-                                                                  ((j) == 0 ? c : 0u));
+#define TFRG_LIN(j)                                                                                       \
+  if (crcw_u & (1u << (j))) lin ^= lin_word<28 - 4 * (j)>(tab, (w[W - 9 + (j)] & cm[W - 9 + (j)]) ^ ((j) == 0 ? c : 0u));
       TFRG_LIN(0) TFRG_LIN(1) TFRG_LIN(2) TFRG_LIN(3) TFRG_LIN(4) TFRG_LIN(5) TFRG_LIN(6) TFRG_LIN(7)
 #undef TFRG_LIN
-      const bool ok = cand && diff == 0u && crc_mask(lin ^ tp[kLtK]) == w[W - 1];
-      const uint64_t okm = __ballot(ok);
-      if (!okm) continue;
-      tsel = ok ? t : tsel;
-      hmask |= 1u << t;
-      hcnt |= (uint32_t)__popcll(okm) << (8u * t);
+      const bool ok = act && diff == 0u && crc_mask(lin ^ meta.y) == w[W - 1];
+      tsel = ok ? cand : tsel;
+      cand = act && !ok ? meta.z : 0xffu;
     }
-    const bool hit = tsel != kTplMax;
+    const bool hit = tsel != 0xffu;
     if (hit) {
       o.status[r] = TFRG_OK;
       o.verdict[r] = (uint8_t)kHitVerdict;
     }
-    if (hmask) {
-      // per slot: each template with hits gives its lanes' order, count word and value / location,
-      // read from its slot table (wave-uniform) and, for inline values, from the window registers
+    if (__ballot(hit)) {
+      const uint32_t* ts = limg + kLiTpl + (hit ? tsel : 0u) * kTw + 4 + 3 * W;  // the lane's slot table
       for (uint32_t k = 0; k < A.n_slots; ++k) {  // (wave-uniform)
-        uint32_t rank = 0, cw = 0, lx = 0, ly = 0, tot = 0;
-        for (uint32_t m = hmask; m; m &= m - 1u) {  // (wave-uniform)
-          const uint32_t t = __builtin_ctz(m);
-          cu32* z = (cu32*)tpl + t * kLtWords + kLtSlot + 3u * k;
-          const uint32_t z0 = z[0], pos = z[1], cwt = z[2];
-          const uint32_t mode = z0 & 0xffu, len = (z0 >> 8) & 0xffu;
-          uint32_t vx = pos, vy = len;  // mode 0: a list's payload-relative location (absent: 0, 0)
-          if (mode == 1u || mode == 2u) {  // one int64 varint / one float: the 4 bytes at window byte pos
-            // (from the window registers, by a wave-uniform register index: a load here would wait
-            // out every store before it, vmcnt)
-            const uint32_t q = pos >> 2;
-            const uint32_t x = __builtin_amdgcn_alignbyte(wsel(w, q + 1u), wsel(w, q), pos & 3u);
-            vx = mode == 1u ? vgroups(x, bytes_mask(len)) : x;
-            vy = 0;
-          } else if (mode == 3u) {  // one bytes element: its batch offset and length
-            vx = en + pos;
+        const uint32_t sq = gimg[kLiSlotQ + k];
+        const u32x4 z = *reinterpret_cast<const u32x4*>(ts + 4u * k);
+        const uint32_t mode = z.x & 0xffu, len = (z.x >> 8) & 0xffu, pos = z.y, cw = z.z;
+        uint32_t lx = pos, ly = len;  // mode 0: a list's payload-relative location (absent: 0, 0)
+        if (sq & kLiQValue) {  // (wave-uniform) one int64 varint / one float: the 4 bytes at window byte pos
+          // (from the window registers -- a load here would wait out every store before it, vmcnt --
+          // over the window words where some template has such a value)
+          const uint32_t qw = pos >> 2;
+          uint32_t a = 0, b = 0;
+          for (uint32_t i = sq & 0xffu; i <= ((sq >> 8) & 0xffu); ++i) {  // (wave-uniform)
+            const bool at = qw == i;
+            a = at ? wsel(w, i) : a;
+            b = at ? wsel(w, i + 1u) : b;
           }
-          const bool sel = tsel == t;
-          rank = sel ? z0 >> 16 : rank;
-          cw = sel ? cwt : cw;
-          lx = sel ? vx : lx;
-          ly = sel ? vy : ly;
-          tot += (cwt & ~kCountInline) * ((hcnt >> (8u * t)) & 0xffu);
+          const uint32_t x = __builtin_amdgcn_alignbyte(b, a, pos & 3u);
+          if (mode == 1u || mode == 2u) {
+            lx = mode == 1u ? vgroups(x, bytes_mask(len)) : x;
+            ly = 0;
+          }
         }
+        if (mode == 3u) lx = en + pos;  // one bytes element: its batch offset and length
+        const uint32_t tot = (sq & kLiQSingle) ? (uint32_t)__popcll(__ballot(hit && cw != 0u))
+                                               : wave_sum(hit ? (cw & ~kCountInline) : 0u);
         const LeanTgt& T = A.tg[k];
         if (hit) {
-          T.ord[r] = (uint16_t)rank;
+          T.ord[r] = (uint16_t)(z.x >> 16);
           if (T.kind) {  // speculative placement: value at column row r; the row split r is implicit
                          // (tfrg_info.placed_slots: a final placement's row splits are never stored)
             if (r < T.lim) {
@@ -287,10 +303,6 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       if (mm) o.rlist[atomicAdd(&o.info[kInfoResid], 1u)] = g;
     }
   };
-  // two groups per step, their windows loaded together: a step waits once, for both windows and
-  // the previous step's column stores (gfx9 counts stores in vmcnt, in issue order), so each wait
-  // covers 128 records; the next step's offsets are requested before this step's stores (they are
-  // then ready without waiting for those)
   auto flush = [&](uint32_t g) {  // the tile sums of group g's tile: the first writer of tsum (zero
     // before the decode; k_lane_count's residual records add theirs with atomics after this kernel)
     if (lane < A.n_slots && acc) {
@@ -301,6 +313,10 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
     acc = 0;
   };
+#if TFRG_TPL_GROUPS_PER_STEP == 2
+  // two groups per step, their windows loaded together: a step waits once, for both windows and
+  // the previous step's column stores (gfx9 counts stores in vmcnt, in issue order), so each wait
+  // covers 128 records; the next step's offsets are requested before this step's stores
   LaneOff f0 = offsets(gbeg), f1 = offsets(gbeg + 1u);
   for (uint32_t g = gbeg; g < gend; g += 2u) {
     wvec wa, wb;
@@ -316,11 +332,24 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       if (((g + 2u) & 3u) == 0u || g + 2u >= gend) flush(g + 1u);
     }
   }
+#else
+  // one group per step (one window live: the per-lane template words need the registers); the next
+  // group's offsets are requested before this group's stores
+  LaneOff f0 = offsets(gbeg);
+  for (uint32_t g = gbeg; g < gend; ++g) {
+    wvec wa;
+    window(wa, f0, g);
+    const LaneOff fa = f0;
+    f0 = offsets(g + 1u);
+    proc(wa, g, fa);
+    if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);
+  }
+#endif
 }
 
 }  // namespace
 
-hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* tpl, uint32_t w,
+hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a, const uint32_t* img, uint32_t w,
                            const uint32_t* d_tab, int num_cus, hipStream_t st) {
   const uint32_t groups = (b.n + 63u) / 64u;
   const uint32_t tiles = (groups + 3u) / 4u;  // (one wave per 256-record tile)
@@ -335,7 +364,8 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   const uint32_t waves = (groups + a2.gpw - 1u) / a2.gpw;
   const dim3 grid(waves ? (waves + kTplBlock / 64 - 1) / (kTplBlock / 64) : 1u);
   const uint32_t* tabs = d_tab + kLeanTabOff;
-#define TFRG_TPL_LAUNCH(WW, OO) hipLaunchKernelGGL((k_tpl_lane<WW, OO>), grid, dim3(kTplBlock), 0, st, b, o, a2, tpl, tabs)
+  const size_t lds = (size_t)a.img_words * 4;  // (the lane image; the CRC tables are static)
+#define TFRG_TPL_LAUNCH(WW, OO) hipLaunchKernelGGL((k_tpl_lane<WW, OO>), grid, dim3(kTplBlock), lds, st, b, o, a2, img, tabs)
 #define TFRG_TPL_OM(WW)                                                        \
   switch (b.omode) {                                                           \
     case kOffU64: TFRG_TPL_LAUNCH(WW, kOffU64); break;                         \

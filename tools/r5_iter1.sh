@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 timeout -k 10 120 tools/bin/probe_lane 16777216 > $O/probe16.txt 2>&1 || { tail $O/probe16.txt; exit 1; }
 cat $O/probe16.txt
 timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread -m gpu \
-  tests/test_templates_gpu.py tests/test_c4_gpu.py tests/test_spec_gpu.py tests/test_gpu_parity.py > $O/tests.log 2>&1 \
+  tests/test_templates_gpu.py tests/test_c4_gpu.py tests/test_spec_gpu.py tests/test_internal_bounds_gpu.py tests/test_gpu_parity.py > $O/tests.log 2>&1 \
   || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for c in c4of8 c4; do
