@@ -57,7 +57,7 @@ def parse_args(argv=None):
     # batch, so the total device memory of a shard is the same
     ap.add_argument("--batch-bytes", type=int, default=1 << 31, help="bytes per decode call of a rank's shard")
     ap.add_argument("--streams", type=int, default=2, help="HIP streams the shard's batches are spread over")
-    ap.add_argument("--only", default=None, choices=["c4", "c1file", "c2", "c3", "c4c2", "c4of8"],
+    ap.add_argument("--only", default=None, choices=["c4", "c1file", "c2", "c3", "c4c2", "c4of8", "c4of8v"],
                     help="measure one config only and report it as the headline (profiling runs)")
     ap.add_argument("--no-extra", action="store_true", help="skip the per-config measurements at N = 1")
     ap.add_argument("--profile-steps", type=int, default=5)
@@ -113,9 +113,10 @@ def c4_workload(shape: str, rank: int, world: int, n_files: int, name: str | Non
     sb = shard.ShardBatch([synth.c4_file_name(f) for f in mine], imgs)
     del imgs
     units = [(int(sb.file_first[i]), int(sb.file_first[i + 1])) for i in range(len(mine))]
-    base = synth.C4_C1_BASE if shape == "c1" else synth.C4_C2_BASE
-    rec = "C1-shaped (int64 label + 12 B bytes_list id)" if shape == "c1" else \
-        "C2-shaped (flowers: lognormal image bytes_list + int64 label + file_name)"
+    base = synth.C4_C2_BASE if shape == "c2" else synth.C4_C1_BASE
+    rec = {"c1": "C1-shaped (int64 label + 12 B bytes_list id)",
+           "c1v": "C1-shaped with variable-length ids (img-{x}, 5-12 B: 16 record shapes)",
+           "c2": "C2-shaped (flowers: lognormal image bytes_list + int64 label + file_name)"}[shape]
     desc = (f"C4 directory (configs[4]) of {n_files} files, {rec} records, {base} +-50 % per file "
             f"(default_rng(1000+f)), spec CRC-32C; this rank's LPT share ({len(mine)} files) resident in HBM")
     w = Workload(name or f"c4_{shape}", desc, sb.buf, sb.starts, sb.ends, units)
@@ -495,6 +496,8 @@ def run(args) -> None:
         w = c4_workload("c1" if only in (None, "c4") else "c2", rank, world, args.files)
     elif only == "c4of8":
         w = c4_workload("c1", 0, 8, args.files, "c4_c1_rank0of8")
+    elif only == "c4of8v":
+        w = c4_workload("c1v", 0, 8, args.files, "c4_c1v_rank0of8")
     else:
         w = single_workload(only)
     head = measure(ctx, w, args.steps, args.warmup, args.profile_steps)
@@ -524,11 +527,13 @@ def run(args) -> None:
         del w
         # c4of8: one rank's share of the same directory at N = 8 (32 of 256 files) decoded alone, the
         # per-GPU work of the 8-GPU strong-scaling point (a weak-scaling reference figure)
-        for name in ("c4of8", "c1file", "c2", "c3", "c4c2"):
+        for name in ("c4of8", "c4of8v", "c1file", "c2", "c3", "c4c2"):
             if name == "c4c2":
                 cw = c4_workload("c2", 0, 1, args.files)
             elif name == "c4of8":
                 cw = c4_workload("c1", 0, 8, args.files, "c4_c1_rank0of8")
+            elif name == "c4of8v":  # the same share with variable-length ids (16 record shapes)
+                cw = c4_workload("c1v", 0, 8, args.files, "c4_c1v_rank0of8")
             else:
                 cw = single_workload(name)
             m = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps)

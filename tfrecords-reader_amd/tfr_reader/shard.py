@@ -267,16 +267,23 @@ class ShardDecoder:
         """Key table and record-shape templates of every batch context from a host sample of the
         first records (device-only callers; the host path learns them itself)."""
         buf = np.asarray(buf).reshape(-1).view(np.uint8)
-        st = np.ascontiguousarray(starts, np.uint64)[:sample]
-        en = np.ascontiguousarray(ends, np.uint64)[:sample]
+        st = np.ascontiguousarray(starts, np.uint64)
+        en = np.ascontiguousarray(ends, np.uint64)
         decs = self._decoders(len(plan))
         if not decs or not st.size:
             return
-        lo, hi = int(st[0]) & ~15, int(en.max())
-        decs[0].decode(buf[lo:hi], st - np.uint64(lo), en - np.uint64(lo))
+        # records spread over the whole shard (its first ones may have shapes the rest has not),
+        # gathered back to back
+        idx = np.unique(np.linspace(0, st.size - 1, min(st.size, sample)).astype(np.int64))
+        s, e = st[idx].astype(np.int64), np.minimum(en[idx], np.uint64(buf.size)).astype(np.int64)
+        e = np.maximum(e, s)
+        part = np.concatenate([buf[a:b] for a, b in zip(s.tolist(), e.tolist())]) if idx.size else buf[:0]
+        pe = np.cumsum(e - s).astype(np.uint64)
+        ps = pe - (e - s).astype(np.uint64)
+        decs[0].decode(part, ps, pe)
         for d in decs:
             d.push_schema()
-            d.learn_templates(buf[lo:hi], st - np.uint64(lo), en - np.uint64(lo))
+            d.learn_templates(part, ps, pe)
 
     def decode_device(self, plan: np.ndarray, d_bytes: int, d_start: int, d_end: int, streams=None,
                       max_record: int | None = None, **kw) -> None:

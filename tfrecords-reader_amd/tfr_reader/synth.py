@@ -99,6 +99,58 @@ def c1_blob(n: int, label_offset: int = 0, id_base: int = 0) -> tuple[np.ndarray
     return blob, offs
 
 
+def _digits(x: np.ndarray) -> np.ndarray:
+    """Decimal digits of non-negative integers (0 has one)."""
+    return 1 + np.searchsorted(10 ** np.arange(1, 19, dtype=np.int64), x, side="right")
+
+
+def c1v_ids(n: int, seed: int) -> np.ndarray:
+    """The ids of ``c1v_blob``: digit counts uniform in [1, 8], values uniform among them."""
+    rng = np.random.default_rng(seed)
+    d = rng.integers(1, 9, n)
+    lo = np.where(d > 1, 10 ** (d - 1), 0)
+    return (lo + (rng.random(n) * (10**d - lo)).astype(np.int64)).astype(np.int64)
+
+
+def c1v_blob(n: int, label_offset: int = 0, seed: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """C1 with variable-length ids: record i has label (label_offset + i) % 1000
+    and id f"img-{x}" without zero padding, x from ``c1v_ids`` (5-12 bytes, uniformly many digits):
+    16 record shapes (8 id lengths x 1-2 label bytes), several of one framed length. Returns
+    (concatenated payloads, offsets[n + 1]); bytes identical to ``writer.encode_example``."""
+    i = np.arange(n, dtype=np.int64)
+    lab = (label_offset + i) % 1000
+    vl = np.where(lab < 128, 1, 2)
+    x = c1v_ids(n, seed)
+    nd = _digits(x)
+    idl = 4 + nd
+    rows = np.zeros((n, 43), np.uint8)
+    head = np.frombuffer(b"\x0a\x00\x0a\x00\x0a\x05label\x12\x00\x1a\x00\x0a\x00", np.uint8)
+    rows[:, :17] = head
+    rows[:, 1] = 27 + vl + idl
+    rows[:, 3] = 13 + vl
+    rows[:, 12] = 4 + vl
+    rows[:, 14] = 2 + vl
+    rows[:, 16] = vl
+    rows[:, 17] = np.where(vl == 1, lab, (lab & 0x7F) | 0x80)
+    rows[:, 18] = lab >> 7
+    tail = np.frombuffer(b"\x0a\x00\x0a\x02id\x12\x00\x0a\x00\x0a\x00img-", np.uint8)
+    rows[:, 19:35] = tail
+    rows[:, 20] = 10 + idl
+    rows[:, 26] = 4 + idl
+    rows[:, 28] = 2 + idl
+    rows[:, 30] = idl
+    for k in range(8):  # digit k (most significant first) at column 35 + k
+        p = nd - 1 - k
+        rows[:, 35 + k] = np.where(p >= 0, 48 + (x // 10 ** np.maximum(p, 0)) % 10, 0)
+    keep = np.ones((n, 43), bool)
+    keep[:, 18] = vl == 2
+    keep[:, 35:] = np.arange(8)[None, :] < nd[:, None]
+    blob = rows[keep]
+    offs = np.zeros(n + 1, np.uint64)
+    np.cumsum(29 + vl + idl, out=offs[1:])
+    return blob, offs
+
+
 def frame_blob(blob: np.ndarray, offs: np.ndarray, crc: bool = True) -> np.ndarray:
     """Frame concatenated payloads (offsets[n + 1]) as TFRecords with the native writer."""
     from tfr_reader import _native as N
@@ -132,7 +184,15 @@ def c4_counts(n_files: int, base: int) -> np.ndarray:
 def c4_file_sizes(n_files: int, shape: str = "c1", base: int | None = None) -> np.ndarray:
     """Framed byte size of every file of the directory, computed without generating it (C1 shape:
     57 bytes + a 1-2 byte label varint per record). C2-shaped sizes need the file's random draws."""
-    counts = c4_counts(n_files, base or (C4_C1_BASE if shape == "c1" else C4_C2_BASE))
+    counts = c4_counts(n_files, base or (C4_C2_BASE if shape == "c2" else C4_C1_BASE))
+    if shape == "c1v":  # 45 + label bytes + id bytes per framed record
+        out = []
+        for f in range(n_files):
+            n = int(counts[f])
+            lab = np.arange(n) % 1000
+            idl = 4 + _digits(c1v_ids(n, 5000 + f))
+            out.append(int((45 + np.where(lab < 128, 1, 2)).sum() + idl.sum()))
+        return np.array(out, np.int64)
     if shape == "c1":
         per_1000 = 128 * 58 + 872 * 59
         full, rem = counts // 1000, counts % 1000
@@ -142,9 +202,12 @@ def c4_file_sizes(n_files: int, shape: str = "c1", base: int | None = None) -> n
 
 def c4_file(f: int, shape: str = "c1", base: int | None = None, crc: bool = True) -> np.ndarray:
     """Framed image of file f of the C4 directory (deterministic in f)."""
-    n = int(c4_counts(f + 1, base or (C4_C1_BASE if shape == "c1" else C4_C2_BASE))[f])
+    n = int(c4_counts(f + 1, base or (C4_C2_BASE if shape == "c2" else C4_C1_BASE))[f])
     if shape == "c1":
         blob, offs = c1_blob(n, 0, f * 1_000_003)
+        return frame_blob(blob, offs, crc)
+    if shape == "c1v":  # C1 with variable-length ids
+        blob, offs = c1v_blob(n, 0, 5000 + f)
         return frame_blob(blob, offs, crc)
     buf, _, _ = framed(c2_payloads(n, seed=1000 + f), crc)
     return buf
