@@ -105,6 +105,8 @@ struct LeanArgs {
   uint32_t img_words;  // the templates' lane image (DevSchema::tpl_img), copied into LDS
   uint32_t gpw;    // (launch_tpl_lane) 64-record groups per wave: 2 (half a tile: small batches,
                    // twice the waves, tile sums added atomically) or a multiple of 4 (whole tiles)
+  uint32_t bsplit; // workgroups from this one on take 2 groups per wave, from group gsplit on (the
+  uint32_t gsplit; // batch's tail in small pieces: the last workgroups dispatched finish together)
   LeanTgt tg[kLeanMaxSlots];
 };
 

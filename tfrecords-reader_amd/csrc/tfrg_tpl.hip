@@ -124,8 +124,9 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   static_assert(kTileShift == 8, "4 groups of 64 records per tile");
   // the wave's groups [gbeg, gend): whole tiles (gpw a multiple of 4, tile sums stored) or half a
   // tile (gpw 2: small batches on twice the waves, tile sums added atomically)
-  const uint32_t gpw = A.gpw;
-  const uint32_t gbeg = (blockIdx.x * kWaves + wib) * gpw;
+  const bool tail = blockIdx.x >= A.bsplit;
+  const uint32_t gpw = tail ? 2u : A.gpw;
+  const uint32_t gbeg = tail ? A.gsplit + ((blockIdx.x - A.bsplit) * kWaves + wib) * 2u : (blockIdx.x * kWaves + wib) * gpw;
   if (gbeg >= ngroups) return;  // (wave-uniform; no barrier follows)
   const uint32_t gend = gbeg + gpw < ngroups ? gbeg + gpw : ngroups;
   const bool whole = (gpw & 3u) == 0u;
@@ -361,8 +362,30 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   // workgroup is L2 traffic)
   LeanArgs a2 = a;
   a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;
-  const uint32_t waves = (groups + a2.gpw - 1u) / a2.gpw;
-  const dim3 grid(waves ? (waves + kTplBlock / 64 - 1) / (kTplBlock / 64) : 1u);
+  // The dispatcher hands out workgroups in index order as slots free up, so the last ones decide
+  // when the batch ends: the groups of about one round of resident workgroups (3 per CU) at the end
+  // of a large batch go to workgroups of 2 groups per wave instead of gpw, and the last round idles
+  // the CUs for a quarter of the time (TFRG_TPL_TAIL=0: off)
+  static const bool split_on = [] {
+    const char* e = getenv("TFRG_TPL_TAIL");
+    return !e || atoi(e) != 0;
+  }();
+  constexpr uint32_t kW = kTplBlock / 64;
+  uint32_t gsplit = groups, bsplit = 0xffffffffu;
+  if (split_on && a2.gpw == 8u) {
+    const uint32_t small = 3u * (uint32_t)num_cus * kW * 2u;  // groups of one round of 2-group workgroups
+    if (groups > 4u * small) {
+      const uint32_t big_blocks = (groups - small) / (kW * a2.gpw);
+      gsplit = big_blocks * kW * a2.gpw;
+      bsplit = big_blocks;
+    }
+  }
+  a2.gsplit = gsplit;
+  a2.bsplit = bsplit;
+  const uint32_t blocks = bsplit != 0xffffffffu
+                              ? bsplit + (groups - gsplit + kW * 2u - 1u) / (kW * 2u)
+                              : ((groups + a2.gpw - 1u) / a2.gpw + kW - 1u) / kW;
+  const dim3 grid(blocks ? blocks : 1u);
   const uint32_t* tabs = d_tab + kLeanTabOff;
   const size_t lds = (size_t)a.img_words * 4;  // (the lane image; the CRC tables are static)
 #define TFRG_TPL_LAUNCH(WW, OO) hipLaunchKernelGGL((k_tpl_lane<WW, OO>), grid, dim3(kTplBlock), lds, st, b, o, a2, img, tabs)
