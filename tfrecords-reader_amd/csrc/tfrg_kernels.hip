@@ -3476,7 +3476,11 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kLaneCountBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
     const int g = per_cu * cfg.num_cus;
-    const int need = (int)(((int64_t)cfg.lane_grid * 256 + kLaneCountBlock - 1) / kLaneCountBlock);
+    int need = (int)(((int64_t)cfg.lane_grid * 256 + kLaneCountBlock - 1) / kLaneCountBlock);
+    // after k_tpl_lane only its missed groups are left: a small batch's residual pass is usually
+    // empty, and dispatching a full grid of workgroups that exit at once costs microseconds (the
+    // grid strides over the listed groups: 4 per wave with this cap)
+    if (lean) need = std::min(need, std::max(8, (int)((b.n + 63u) / 64u / 16u)));
     return g < need || !cap ? g : need;
   };
   if (lane_lds <= kLaneLdsBudget) {
@@ -3512,7 +3516,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTailBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
-    const uint32_t g = (uint32_t)(per_cu * cfg.num_cus);
+    // (a small batch: fewer workgroups -- both roles stride -- so that an empty launch, the usual case
+    // of batches of small records, is not a full grid of dispatches)
+    const uint32_t g = std::min((uint32_t)(per_cu * cfg.num_cus), std::max(8u, (uint32_t)(b.nbytes >> 16) + b.n / 4096u));
     if (gord)
       hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab, d_consts,
                          cfg.lane_max);
@@ -3534,7 +3540,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     // placement strides over the tiles)
     bool all_spec = scx.spec && cfg.spec_h && S <= 64;
     for (size_t k = 0; all_spec && k < S; ++k) all_spec = cfg.spec_h[k] != 0u;
-    const uint32_t resident = (all_spec ? 1u : 8u) * (uint32_t)cfg.num_cus;
+    // (all placed: usually nothing to do but the launch; a small batch also strides with fewer)
+    const uint32_t resident = all_spec ? std::min((uint32_t)cfg.num_cus, std::max(8u, n_tiles / 4u)) : 8u * (uint32_t)cfg.num_cus;
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus) {
       const uint32_t ng = (n_tiles + 3) / 4;
       hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3(ng < resident ? ng : resident), dim3(kLaneBlock), 0, st, b,
@@ -3551,7 +3558,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     int per_cu = 0;  // one round of resident workgroups (3 per CU: a second round would run at 1/3)
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kWaveBlock, lds) != hipSuccess || per_cu < 1)
       per_cu = 1;
-    const int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
+    int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
+    // (a small batch: its roles stride over fewer waves; large records keep the full grid)
+    g = (int)std::min<uint64_t>((uint64_t)g, std::max<uint64_t>(8u, std::max<uint64_t>(b.n / 1024u, b.nbytes >> 16)));
     hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, ox, cfg.lane_max);
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)

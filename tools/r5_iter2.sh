@@ -12,8 +12,10 @@ timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method threa
   tests/test_c4_gpu.py tests/test_gpu_parity.py > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 for c in c4of8 c4of8v; do
-  for L in libtfrg.so libtfrg_v3g2.so libtfrg_v2.so; do
-    TFRG_LIB=$PWD/tfrecords-reader_amd/tfr_reader/$L timeout -k 10 300 python bench.py --only $c --no-cpu --steps 20 > $O/b_${c}_$L.json 2> $O/b_${c}_$L.err || { tail -30 $O/b_${c}_$L.err; exit 1; }
+  for L in libtfrg.so libtfrg_v3g2.so libtfrg_v2.so notail; do
+    E=""; LL=$L
+    if [ $L = notail ]; then E="TFRG_TPL_TAIL=0"; LL=libtfrg.so; fi
+    env $E TFRG_LIB=$PWD/tfrecords-reader_amd/tfr_reader/$LL timeout -k 10 300 python bench.py --only $c --no-cpu --steps 20 > $O/b_${c}_$L.json 2> $O/b_${c}_$L.err || { tail -30 $O/b_${c}_$L.err; exit 1; }
     python3 - "$O/b_${c}_$L.json" "$c $L" <<'PY'
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])

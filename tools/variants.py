@@ -13,6 +13,11 @@ REPO = Path(__file__).resolve().parents[1]
 CS = REPO / "tfrecords-reader_amd" / "csrc"
 
 VARIANTS = {
+    # k_tail_count in 1024-thread workgroups, one per CU (the streaming CRC's 70 KiB of LDS tables
+    # loaded 256 times instead of 512; the same 16 waves per CU)
+    "tail1024": [("tfrg_kernels.hip", "constexpr uint32_t kTailBlock = 512;", "constexpr uint32_t kTailBlock = 1024;"),
+                 ("tfrg_kernels.hip", "__global__ __launch_bounds__(kTailBlock, 2) void k_tail_count",
+                  "__global__ __launch_bounds__(kTailBlock, 4) void k_tail_count")],
     # k_tpl_lane without its column stores (read side alone; wrong results)
     "nostore": [("tfrg_tpl.hip", "      if (ok) {\n        o.status[r] = TFRG_OK;",
                  "      if (ok && A.n_tpl > 99) {\n        o.status[r] = TFRG_OK;"),
