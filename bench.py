@@ -305,6 +305,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         elapsed = float(t.item())
     infos = sd.infos(plan)
     _check(infos)
+    dev_bytes, reruns = sd.device_bytes()
 
     # ---- per-kernel durations: HIP events recorded by libtfrg on the launch stream, the batches
     # run back to back on one stream so that no launch overlaps another batch's
@@ -376,6 +377,10 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         "batches": launches,
         "batch_bytes_max": int((plan[:, 3] - plan[:, 2]).max()),
         "offsets": {"mode": omode, "bytes_per_record": off_bytes},
+        # device memory of the decode contexts (value columns sized from the learning sample), and
+        # of the resident input, in multiples of the input
+        "device_memory": {"contexts_bytes": dev_bytes, "x_input": round(dev_bytes / max(nbytes, 1), 3),
+                          "worst_case_reruns": reruns},
         "streams": len(handles),
         "ms_per_step": round(ms_step, 4),
         "GiB_s": round(framed / (ms_step / 1e3) / 2**30, 3),

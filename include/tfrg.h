@@ -113,6 +113,14 @@ int tfrg_ctx_set_lane_max(tfrg_ctx* ctx, uint32_t lane_max);
  * kernel is not launched (a few microseconds per decode); a wrong bound still decodes correctly
  * (such records take the lane kernel's slower path). tfrg_decode_host derives it per call. */
 int tfrg_ctx_set_record_bound(tfrg_ctx* ctx, uint64_t max_record_bytes);
+/* Value-capacity hints: the int64 / float / bytes_list values the following decodes are expected to
+ * produce at most (0 = unknown, the default: the worst case one int64 per input byte, one float per
+ * 4 bytes, one bytes element per 2 -- about 13 x the batch's bytes of device memory). A decode whose
+ * values exceed a hint is re-run with the worst case inside tfrg_result_info before it returns (the
+ * results are always complete); tfrg_ctx_device_bytes counts those re-runs. */
+int tfrg_ctx_set_value_caps(tfrg_ctx* ctx, uint64_t int64_values, uint64_t float_values, uint64_t bytes_values);
+/* device memory held by the context (bytes) and the decodes re-run because a hint was too small */
+int tfrg_ctx_device_bytes(tfrg_ctx* ctx, uint64_t* bytes, uint64_t* hint_reruns);
 /* wavefront records spanning <= nbytes are staged in LDS (clamped to the kernel's 12 KiB stage;
  * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
 int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);

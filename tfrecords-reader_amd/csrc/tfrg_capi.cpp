@@ -72,6 +72,16 @@ const CrcTables& crc_tables() {
 
 using namespace tfrg;
 
+// record offsets of one decode call (DevBatch: u64 pairs, u32 pairs, or u32 ends of back-to-back records)
+struct Offsets {
+  const uint64_t* s64 = nullptr;
+  const uint64_t* e64 = nullptr;
+  const uint32_t* s32 = nullptr;
+  const uint32_t* e32 = nullptr;
+  uint32_t first = 0;
+  uint32_t mode = kOffU64;
+};
+
 struct tfrg_ctx {
   int device = 0;
   hipStream_t own_stream = nullptr;
@@ -131,6 +141,21 @@ struct tfrg_ctx {
   bool profiling = false;
   bool have_events = false;
   hipEvent_t ev[kNumStages + 1] = {};
+  // value-capacity hints (tfrg_ctx_set_value_caps; 0: the worst case) and the last decode's
+  // arguments, for the transparent worst-case re-run when a hint proved too small
+  uint64_t hint_i64 = 0, hint_f32 = 0, hint_b = 0;
+  bool hinted = false;  // the last decode ran with a hint below its worst case
+  bool no_hints = false;  // (the re-run: the worst case)
+  uint64_t hint_reruns = 0;  // decodes re-run because a hint was too small
+  struct LastCall {
+    const uint8_t* d_bytes;
+    uint64_t nbytes;
+    uint64_t cap_in;
+    uint64_t bound;
+    uint32_t n, flags;
+    hipStream_t st;
+  } last{};
+  Offsets last_off{};
   // debug hook: records whose list locations are poisoned after the count passes (tests)
   uint32_t poison[4] = {0xffffffffu, 0xffffffffu, 0xffffffffu, 0xffffffffu};
 };
@@ -241,6 +266,30 @@ int tfrg_ctx_set_lane_max(tfrg_ctx* c, uint32_t lane_max) {
 int tfrg_ctx_set_record_bound(tfrg_ctx* c, uint64_t max_record_bytes) {
   if (!c) return TFRG_E_ARG;
   c->record_bound = max_record_bytes;
+  return 0;
+}
+
+int tfrg_ctx_set_value_caps(tfrg_ctx* c, uint64_t int64_values, uint64_t float_values, uint64_t bytes_values) {
+  if (!c) return TFRG_E_ARG;
+  c->hint_i64 = int64_values;
+  c->hint_f32 = float_values;
+  c->hint_b = bytes_values;
+  return 0;
+}
+
+int tfrg_ctx_device_bytes(tfrg_ctx* c, uint64_t* bytes, uint64_t* reruns) {
+  if (!c) return TFRG_E_ARG;
+  const DBuf* all[] = {&c->crc_tab, &c->consts, &c->ht, &c->key_hash, &c->key_off, &c->key_blob, &c->key_slot,
+                       &c->slot_kind, &c->key_w, &c->krec, &c->in_bytes, &c->in_start, &c->in_end, &c->status,
+                       &c->aux, &c->verdict, &c->order, &c->count, &c->loc, &c->rs, &c->ident, &c->slot_base,
+                       &c->totals, &c->kind_totals, &c->i64, &c->f32, &c->b_off, &c->b_len, &c->big_list,
+                       &c->slow_list, &c->miss, &c->info, &c->tsum, &c->bdata, &c->boff64, &c->blb, &c->bbig,
+                       &c->crc_rec, &c->crc_base, &c->crc_part, &c->tpl, &c->spec, &c->dq, &c->dq_cnt, &c->lmask,
+                       &c->rlist};
+  uint64_t t = 0;
+  for (const DBuf* b : all) t += b->cap;
+  if (bytes) *bytes = t;
+  if (reruns) *reruns = c->hint_reruns;
   return 0;
 }
 
@@ -767,16 +816,6 @@ extern "C" int tfrg_ctx_set_templates(tfrg_ctx* c, int on) {
   return 0;
 }
 
-// record offsets of one decode call (DevBatch: u64 pairs, u32 pairs, or u32 ends of back-to-back records)
-struct Offsets {
-  const uint64_t* s64 = nullptr;
-  const uint64_t* e64 = nullptr;
-  const uint32_t* s32 = nullptr;
-  const uint32_t* e32 = nullptr;
-  uint32_t first = 0;
-  uint32_t mode = kOffU64;
-};
-
 static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const Offsets& off, uint32_t n,
                              uint32_t flags, void* stream);
 
@@ -834,7 +873,21 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   // of overlapping device ranges that exceeds them is reported by tfrg_result_info (TFRG_E_LIMIT).
   const uint64_t cap_in = c->cap_hint > nbytes ? c->cap_hint : nbytes;
   c->cap_hint = 0;
-  const uint64_t cap_i64 = cap_in + 16, cap_f32 = cap_in / 4 + 16, cap_b = cap_in / 2 + 16;
+  uint64_t cap_i64 = cap_in + 16, cap_f32 = cap_in / 4 + 16, cap_b = cap_in / 2 + 16;
+  // value-capacity hints (tfrg_ctx_set_value_caps) below the worst case: a decode that overflows one
+  // is re-run with the worst case by tfrg_result_info (decode_rerun), before any result is read
+  c->hinted = false;
+  auto hint = [&](uint64_t h, uint64_t& cap) {
+    if (h && h + 16 < cap) {
+      cap = h + 16;
+      c->hinted = true;
+    }
+  };
+  if (!c->no_hints) {
+    hint(c->hint_i64, cap_i64);
+    hint(c->hint_f32, cap_f32);
+    hint(c->hint_b, cap_b);
+  }
   // growing an arena buffer frees the old one: wait for work that may still read it
   bool grow = c->status.cap < nn * 4 || c->aux.cap < nn * 8 || c->verdict.cap < nn ||
               c->order.cap < S * nn * 2 || c->count.cap < S * nn * 4 || c->loc.cap < S * nn * 8 ||
@@ -949,6 +1002,8 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   memcpy(cfg.poison, c->poison, sizeof(cfg.poison));
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
+  c->last = tfrg_ctx::LastCall{d_bytes, nbytes, cap_in, bound, n, flags, st};
+  c->last_off = off;
   // deferred packed bodies when records above lane_max may be walked from HBM: one 64-row block
   // (2,048 entries of 16 bytes) per 256 KiB of input, at least 16
   o.dq = nullptr;
@@ -1058,10 +1113,23 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   HIP_TRY(hipSetDevice(c->device));
   uint32_t h[kInfoCount] = {0};
   uint64_t kt[4] = {0, 0, 0, 0};
-  HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, sizeof(h), hipMemcpyDeviceToHost,
-                         c->last_stream));
-  HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
-  HIP_TRY(hipStreamSynchronize(c->last_stream));
+  for (int attempt = 0;; ++attempt) {
+    HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, sizeof(h), hipMemcpyDeviceToHost,
+                           c->last_stream));
+    HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    if (!h[kInfoOverflow] || !c->hinted || attempt) break;
+    // a value-capacity hint was too small for this batch: the same decode again with the worst-case
+    // capacities (its inputs are still the caller's: the decode has not been reported complete)
+    const tfrg_ctx::LastCall L = c->last;
+    c->no_hints = true;
+    c->cap_hint = L.cap_in;
+    c->call_bound = L.bound;
+    const int rc = decode_device_any(c, L.d_bytes, L.nbytes, c->last_off, L.n, L.flags, L.st);
+    c->no_hints = false;
+    if (rc) return rc;
+    ++c->hint_reruns;
+  }
   uint64_t blen = 0;
   if (c->materialized && !h[kInfoOverflow]) {  // the byte column's length: offsets[nb]
     const uint64_t nb = c->n ? kt[TFRG_KIND_BYTES] : 0;

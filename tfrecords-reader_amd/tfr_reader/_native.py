@@ -126,6 +126,8 @@ SIGNATURES: dict[str, tuple] = {
     "tfrg_stream_result": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(TfrgInfo), C.POINTER(TfrgColumns)]),
     "tfrg_stream_host_ranges": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(u64p), C.POINTER(u64p)]),
     "tfrg_ctx_set_profiling": (C.c_int, [C.c_void_p, C.c_int]),
+    "tfrg_ctx_set_value_caps": (C.c_int, [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "tfrg_ctx_device_bytes": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "tfrg_profile_last": (C.c_int, [C.c_void_p, C.POINTER(C.c_float), C.POINTER(C.c_char_p), C.c_int]),
     "tfrg_set_schema": (
         C.c_int,

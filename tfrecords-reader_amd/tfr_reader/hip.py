@@ -234,6 +234,19 @@ class HipDecoder:
         N.check(self._lib.tfrg_result_info(self._ctx, C.byref(info)), "tfrg_result_info")
         return info
 
+    def set_value_caps(self, int64_values: int = 0, float_values: int = 0, bytes_values: int = 0) -> None:
+        """Capacity hints for the values of the following decodes (0: the worst case, ~13x the
+        batch bytes of device memory); a decode that exceeds one is re-run with the worst case inside
+        ``info()`` (tfrg_ctx_set_value_caps)."""
+        N.check(self._lib.tfrg_ctx_set_value_caps(self._ctx, int(int64_values), int(float_values), int(bytes_values)),
+                "tfrg_ctx_set_value_caps")
+
+    def device_bytes(self) -> tuple[int, int]:
+        """(device memory held by this decoder's context, decodes re-run because a hint was too small)."""
+        b, r = C.c_uint64(), C.c_uint64()
+        N.check(self._lib.tfrg_ctx_device_bytes(self._ctx, C.byref(b), C.byref(r)), "tfrg_ctx_device_bytes")
+        return int(b.value), int(r.value)
+
     def device_columns(self) -> N.TfrgColumns:
         """Device pointers of the last result (tfrg_result_device): valid until the next decode on
         this decoder; the placed slots' identity row splits are written into them on the decode's

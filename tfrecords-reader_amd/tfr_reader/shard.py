@@ -182,10 +182,11 @@ class ShardDecoder:
     pool over files (indexer.py:121-134) and a thread pool over records (reader.py:212-247)."""
 
     def __init__(self, device: int = 0, batch_bytes: int = DEFAULT_BATCH_BYTES, n_streams: int = 2,
-                 spec_varint: bool = False, keys=None) -> None:
+                 spec_varint: bool = False, keys=None, value_caps: bool = True) -> None:
         from tfr_reader import hip
 
         self.device = device
+        self.value_caps = value_caps  # learn(): size the value columns from the sample
         self.batch_bytes = int(batch_bytes)
         self.n_streams = max(1, int(n_streams))
         self.spec_varint = spec_varint
@@ -280,10 +281,19 @@ class ShardDecoder:
         part = np.concatenate([buf[a:b] for a, b in zip(s.tolist(), e.tolist())]) if idx.size else buf[:0]
         pe = np.cumsum(e - s).astype(np.uint64)
         ps = pe - (e - s).astype(np.uint64)
-        decs[0].decode(part, ps, pe)
-        for d in decs:
+        r = decs[0].decode(part, ps, pe)
+        # value capacities from the sample's values per input byte (x 1.25 + 64 Ki): the batches'
+        # value columns sized to their data instead of the worst case (one int64 per byte: ~13x the
+        # input); a batch that exceeds them is re-decoded with the worst case (HipDecoder.info)
+        kt = [int(x) for x in r.info.kind_totals]
+        per = max(int(part.size), 1)
+        for k, d in enumerate(decs):
             d.push_schema()
             d.learn_templates(part, ps, pe)
+            if self.value_caps and k < len(plan):
+                nb = int(plan[k, 3] - plan[k, 2])
+                caps = [int(kt[j] * nb / per * 1.25) + 65536 for j in (3, 2, 1)]
+                d.set_value_caps(*caps)
 
     def decode_device(self, plan: np.ndarray, d_bytes: int, d_start: int, d_end: int, streams=None,
                       max_record: int | None = None, **kw) -> None:
@@ -311,6 +321,14 @@ class ShardDecoder:
             s = streams[k % len(streams)] if streams else None
             decs[k].decode_device32(d_bytes + lo, hi - lo, d_start32 + 4 * r0 if d_start32 else None, d_end32 + 4 * r0,
                                     int(firsts[k]), r1 - r0, stream=s, **kw)
+
+    def device_bytes(self) -> tuple[int, int]:
+        """(device memory of every batch context, worst-case re-runs so far)."""
+        b = r = 0
+        for d in self.decs:
+            x, y = d.device_bytes()
+            b, r = b + x, r + y
+        return b, r
 
     def infos(self, plan: np.ndarray) -> list:
         """Decode summaries of the last ``decode_device`` (waits for it)."""
