@@ -423,7 +423,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
                                        mean_launch_ms=round(tr[dominant] / launches, 5),
                                        frac_of_guide_copy=round(achieved / GUIDE_COPY_GBS, 4),
                                        timing="rocprofv3 kernel trace (" + out["kernels_ms_trace_source"] + ")")
-    traffic = _traffic(w, dominant, launches)
+    traffic = _traffic(w, dominant, launches, omode)
     if traffic:
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic
     sd.close()
@@ -438,7 +438,7 @@ def _present_lists(dec, w: Workload) -> float:
     return float((r.order != 0).sum()) * w.n / k
 
 
-def _traffic(w: Workload, kernel: str, launches: int):
+def _traffic(w: Workload, kernel: str, launches: int, omode: str = "u64"):
     """HBM bytes per launch of the dominant kernel from the committed PMC passes of THIS workload
     (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM): only when the
     profile names the same workload, record count and batch count, else None."""
@@ -446,7 +446,8 @@ def _traffic(w: Workload, kernel: str, launches: int):
     if not tf.is_file():
         return None
     t = json.loads(tf.read_text())
-    if kernel not in t.get("kernel", "") or t.get("records") != w.n or t.get("launches_per_step") != launches:
+    if kernel not in t.get("kernel", "") or t.get("records") != w.n or t.get("launches_per_step") != launches or \
+            t.get("offsets", "u64") != omode:
         return None
     return int(t["traffic_bytes"]), f"profiles/{tf.name}"
 
@@ -587,6 +588,8 @@ def run(args) -> None:
             "batch_bytes_max": head["batch_bytes_max"],
             "streams": head["streams"],
             "tpl_groups_missed": head["tpl_groups_missed"],
+            "offsets": head["offsets"],
+            "device_memory": head["device_memory"],
         }
         if meta:
             cfg.update(files_total=meta["files_total"], files_per_gpu=meta["files_mine"],

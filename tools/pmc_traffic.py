@@ -43,10 +43,11 @@ def main() -> None:
     out.mkdir(parents=True, exist_ok=True)
     name, fetch_kb = per_launch(run_pass(out, "FETCH_SIZE", config), want)
     _, write_kb = per_launch(run_pass(out, "WRITE_SIZE", config), want)
-    workload = {"c4": "c4_c1", "c4c2": "c4_c2", "c4of8": "c4_c1_rank0of8"}.get(config, config)
+    workload = {"c4": "c4_c1", "c4c2": "c4_c2", "c4of8": "c4_c1_rank0of8", "c4of8v": "c4_c1v_rank0of8"}.get(config, config)
     line = json.loads((out / "FETCH_SIZE.log").read_text().strip().splitlines()[-1])
     records, launches = line["config"]["records_per_gpu"], line["config"]["batches_per_gpu"]
     res = {"config": workload, "records": records, "launches_per_step": launches,
+           "offsets": line["config"].get("offsets", {}).get("mode", "u64"),
            "kernel": name.replace("(anonymous namespace)::", "").split("(")[0], "fetch_size_kb": fetch_kb,
            "write_size_kb": write_kb,
            "traffic_bytes": fetch_kb * 1024 * 2 + write_kb * 1024,
