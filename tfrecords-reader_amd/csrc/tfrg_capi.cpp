@@ -130,6 +130,7 @@ struct tfrg_ctx {
   uint32_t tpl_img_words = 0;
   std::vector<uint32_t> tpl_h;  // host copy of the template words
   bool tpl_learned = false;
+  bool tpl_full = false;  // the templates took every record of their learning sample
   bool tpl_on = true;
   // speculative single-value placement (DevSchema::spec), derived from the templates
   std::vector<uint8_t> slot_kind_h;
@@ -556,6 +557,7 @@ struct Learned {
   std::vector<uint32_t> w, spec, img;  // window-form templates, spec words, lane image
   uint32_t W = 0;
   bool have_spec = false;
+  bool full = false;  // every sampled record took a kept template
 };
 uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                       const uint64_t* h_end, uint32_t n, uint32_t flags, Learned& out) {
@@ -590,6 +592,9 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
   std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
   const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMaxLane);
   if (!nt) return 0;
+  uint64_t kept = 0;
+  for (uint32_t k = 0; k < nt; ++k) kept += order[k].first;
+  out.full = kept == lim;
   // speculative placement (DevSchema::spec): slots that are an inline single value in every kept
   // template, taken per kind in slot order up to the first slot of that kind that is not one (its
   // column base n * rank then holds whenever every record is regular)
@@ -772,6 +777,7 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   c->tpl_h = w;
   c->spec_h = spec;
   c->have_spec = have_spec;
+  c->tpl_full = L.full;
   return (int)nt;
 }
 
@@ -990,6 +996,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   LaunchCfg cfg;
   cfg.num_cus = c->num_cus;
   cfg.lean = c->tpl_on && c->n_tpl;
+  cfg.tpl_full = cfg.lean && c->tpl_full;
   cfg.spec_h = c->spec_h.empty() ? nullptr : c->spec_h.data();
   const uint64_t lane_blocks = (n + 255) / 256;
   const uint64_t lane_cap = (uint64_t)c->num_cus * 8;

@@ -289,6 +289,8 @@ uint64_t materialize_lb_words(uint64_t cap_b);
 struct LaunchCfg {
   int num_cus;
   bool lean;               // k_tpl_lane first (window-form templates, framed records with CRCs)
+  bool tpl_full;           // the templates took their whole learning sample (the later passes are
+                           // then usually empty: launched with small grids)
   const uint32_t* spec_h;  // host copy of DevSchema::spec (k_tpl_lane's placement targets)
   int lane_grid;           // cap: workgroups for one record per lane
   int wave_grid;

@@ -3432,6 +3432,11 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   const bool lean = cfg.lean && sc.n_tpl && fast_ok && S <= kLeanMaxSlots && o.lmask && o.rlist &&
                     (sc.tpl_w == 16 || sc.tpl_w == 32 || sc.tpl_w == 64) &&
                     !(b.flags & (kFlagPayloadOnly | kFlagNoCrc)) && b.nbytes < 0xffffff00ull;
+  // every record of the learning sample took a template and none is above lane_max: the passes after
+  // k_tpl_lane (residual lane records, slow walks, large-record CRCs, gathers of placed slots) are
+  // usually empty, and a full grid of workgroups that exit at once costs ~4 us per launch; they
+  // run with small grids instead (any work they do find is still done: every one strides)
+  const bool quiet = lean && cfg.tpl_full && !cfg.body_count;
   DevOut ox = o;
   if (!lean) {
     ox.lmask = nullptr;
@@ -3481,6 +3486,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     // empty, and dispatching a full grid of workgroups that exit at once costs microseconds (the
     // grid strides over the listed groups: 4 per wave with this cap)
     if (lean) need = std::min(need, std::max(8, (int)((b.n + 63u) / 64u / 16u)));
+    if (quiet) need = std::min(need, 64);
     return g < need || !cap ? g : need;
   };
   if (lane_lds <= kLaneLdsBudget) {
@@ -3518,7 +3524,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       per_cu = 1;
     // (a small batch: fewer workgroups -- both roles stride -- so that an empty launch, the usual case
     // of batches of small records, is not a full grid of dispatches)
-    const uint32_t g = std::min((uint32_t)(per_cu * cfg.num_cus), std::max(8u, (uint32_t)(b.nbytes >> 16) + b.n / 4096u));
+    uint32_t g = std::min((uint32_t)(per_cu * cfg.num_cus), std::max(8u, (uint32_t)(b.nbytes >> 16) + b.n / 4096u));
+    if (!cfg.body_count) g = std::min(g, 32u);  // (no record above lane_max: role 2 has nothing to stream)
     if (gord)
       hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab, d_consts,
                          cfg.lane_max);
@@ -3541,7 +3548,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     bool all_spec = scx.spec && cfg.spec_h && S <= 64;
     for (size_t k = 0; all_spec && k < S; ++k) all_spec = cfg.spec_h[k] != 0u;
     // (all placed: usually nothing to do but the launch; a small batch also strides with fewer)
-    const uint32_t resident = all_spec ? std::min((uint32_t)cfg.num_cus, std::max(8u, n_tiles / 4u)) : 8u * (uint32_t)cfg.num_cus;
+    uint32_t resident = all_spec ? std::min((uint32_t)cfg.num_cus, std::max(8u, n_tiles / 4u)) : 8u * (uint32_t)cfg.num_cus;
+    if (all_spec && quiet) resident = std::min(resident, 32u);
     if (n_tiles >= 16u * (uint32_t)cfg.num_cus) {
       const uint32_t ng = (n_tiles + 3) / 4;
       hipLaunchKernelGGL((k_down_gather<COMPAT, 4>), dim3(ng < resident ? ng : resident), dim3(kLaneBlock), 0, st, b,
@@ -3552,6 +3560,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     }
   }
   mark(kStageTailGather);
+  bool all_spec_t = scx.spec && cfg.spec_h && S <= 64;
+  for (size_t k = 0; all_spec_t && k < S; ++k) all_spec_t = cfg.spec_h[k] != 0u;
   if (S > 0) {  // the gathers after the scan: lane records' lists, staged and huge large records
     const size_t lds = (size_t)kWRegion * kWavesPerBlock;
     const void* fn = reinterpret_cast<const void*>(&k_tail_gather<COMPAT>);
@@ -3561,6 +3571,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     int g = per_cu * cfg.num_cus < cfg.wave_grid ? per_cu * cfg.num_cus : cfg.wave_grid;
     // (a small batch: its roles stride over fewer waves; large records keep the full grid)
     g = (int)std::min<uint64_t>((uint64_t)g, std::max<uint64_t>(8u, std::max<uint64_t>(b.n / 1024u, b.nbytes >> 16)));
+    if (quiet && all_spec_t) g = std::min(g, 32);
     hipLaunchKernelGGL((k_tail_gather<COMPAT>), dim3(g), dim3(kWaveBlock), lds, st, b, scx, ox, cfg.lane_max);
   }
   mark(kStageMaterialize);  // (the caller launches the optional materialize pass and marks the end)

@@ -3,7 +3,7 @@
 between the launches: the per-stage events bench.py records inflate sub-10-us kernels ~2x).
 
 usage: kernel_trace.py <outdir> <only> [steps]
-Runs ``rocprofv3 --kernel-trace`` over ``bench.py --only <only> --no-cpu --steps S --profile-steps 0``
+Runs ``rocprofv3 --kernel-trace`` over ``bench.py --only <only> --no-cpu --steps S --profile-steps 1``
 and writes profiles-style JSON: the mean duration of each decode kernel over its last S x batches
 launches (the timed steps; earlier ones are the learning sample and the warmup), and their sum per
 step. bench.py reads ``profiles/kernels_<workload>.json`` for a workload of the same record count
@@ -27,10 +27,10 @@ def main() -> None:
     out.mkdir(parents=True, exist_ok=True)
     cmd = ["timeout", "-s", "KILL", "300", "rocprofv3", "--kernel-trace", "--output-format", "csv", "-d", str(out),
            "-o", "run", "--", sys.executable, str(REPO / "bench.py"), "--only", only, "--no-cpu", "--steps",
-           str(steps), "--profile-steps", "0", "--warmup", "3"]
-    with open(out / "run.log", "w") as log:
-        subprocess.run(cmd, check=True, stdout=log, stderr=subprocess.STDOUT, env=dict(os.environ, TMPDIR="/tmp"))
-    line = json.loads((out / "run.log").read_text().strip().splitlines()[-1])
+           str(steps), "--profile-steps", "1", "--warmup", "3"]
+    with open(out / "run.log", "w") as log, open(out / "run.err", "w") as err:
+        subprocess.run(cmd, check=True, stdout=log, stderr=err, env=dict(os.environ, TMPDIR="/tmp"))
+    line = next(json.loads(x) for x in reversed((out / "run.log").read_text().splitlines()) if x.startswith('{"metric"'))
     batches = int(line["config"]["batches_per_gpu"])
     rows = list(csv.DictReader(open(next(out.rglob("*kernel_trace.csv")))))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
@@ -40,8 +40,9 @@ def main() -> None:
         base = next((k for k in DECODE if k in name), None)
         if base:
             per[base].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    # (the last decode of each batch is bench.py's profiling step, with HIP events: dropped)
     k = steps * batches
-    us = {name: sum(d[-k:]) / steps for name, d in per.items() if len(d) >= k}
+    us = {name: sum(d[-k - batches : -batches]) / steps for name, d in per.items() if len(d) >= k + batches}
     res = {"only": only, "workload": line["config"]["workload"], "records": line["config"]["records_per_gpu"],
            "steps": steps, "batches": batches, "kernels_us_per_step": {n: round(v, 2) for n, v in us.items()},
            "kernels_sum_us": round(sum(us.values()), 2), "bench_ms_per_step": line["ms_per_step"]}
