@@ -3482,10 +3482,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
       per_cu = 1;
     const int g = per_cu * cfg.num_cus;
     int need = (int)(((int64_t)cfg.lane_grid * 256 + kLaneCountBlock - 1) / kLaneCountBlock);
-    // after k_tpl_lane only its missed groups are left: a small batch's residual pass is usually
-    // empty, and dispatching a full grid of workgroups that exit at once costs microseconds (the
-    // grid strides over the listed groups: 4 per wave with this cap)
-    if (lean) need = std::min(need, std::max(8, (int)((b.n + 63u) / 64u / 16u)));
+    // (after a template pass that took its whole sample the residual pass is usually empty; it
+    // strides over whatever groups it finds. Not for records above lane_max: k_tpl_lane leaves
+    // every one of them, and walking them is this pass's work)
     if (quiet) need = std::min(need, 64);
     return g < need || !cap ? g : need;
   };

@@ -2,7 +2,7 @@
 # round-5 GPU pass 3: C2 with the tail-count kernel in 1024-thread workgroups, C3 cut into batches on
 # two streams (batch-bytes), configs[1]
 set -u
-O=gpurun_out/r5c; mkdir -p $O
+O=gpurun_out/r5f/c23; mkdir -p $O
 export TMPDIR=/tmp
 line() {
   python3 - "$1" "$2" <<'PY'

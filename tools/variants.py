@@ -13,6 +13,23 @@ REPO = Path(__file__).resolve().parents[1]
 CS = REPO / "tfrecords-reader_amd" / "csrc"
 
 VARIANTS = {
+    # k_tpl_lane: one tile (4 groups) per wave on large batches instead of two
+    "t1": [("tfrg_tpl.hip", "a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;",
+            "a2.gpw = need < (uint32_t)num_cus ? 2u : 4u;"),
+           ("tfrg_tpl.hip", "if (split_on && a2.gpw == 8u) {", "if (split_on && a2.gpw >= 4u) {")],
+    # k_tpl_lane: two groups per step (both windows loaded together) at 5 waves/SIMD (96 VGPRs)
+    "g2lb5": [("tfrg_tpl.hip", "#define TFRG_TPL_GROUPS_PER_STEP 1", "#define TFRG_TPL_GROUPS_PER_STEP 2"),
+              ("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
+               "__launch_bounds__(kTplBlock, W == 16 ? 5 : (W == 32 ? 4 : 2))")],
+    "t1g2lb5": [("tfrg_tpl.hip", "a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;",
+                 "a2.gpw = need < (uint32_t)num_cus ? 2u : 4u;"),
+                ("tfrg_tpl.hip", "if (split_on && a2.gpw == 8u) {", "if (split_on && a2.gpw >= 4u) {"),
+                ("tfrg_tpl.hip", "#define TFRG_TPL_GROUPS_PER_STEP 1", "#define TFRG_TPL_GROUPS_PER_STEP 2"),
+                ("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
+                 "__launch_bounds__(kTplBlock, W == 16 ? 5 : (W == 32 ? 4 : 2))")],
+    # k_tpl_lane at 8 waves/SIMD (64 VGPRs)
+    "lb8v3": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
+               "__launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2))")],
     # k_tail_count in 1024-thread workgroups, one per CU (the streaming CRC's 70 KiB of LDS tables
     # loaded 256 times instead of 512; the same 16 waves per CU)
     "tail1024": [("tfrg_kernels.hip", "constexpr uint32_t kTailBlock = 512;", "constexpr uint32_t kTailBlock = 1024;"),
