@@ -37,7 +37,8 @@ struct Cols {
   uint32_t* sink;
 };
 
-enum : int { kU64 = 1, kStore = 2, kPipe = 4, kCheck = 8 };
+enum : int { kU64 = 1, kStore = 2, kPipe = 4, kCheck = 8, kNoSV = 16, kNoOrd = 32, kStaged = 64, kTabLds = 128,
+             kTab8 = 256 };
 
 template <int MODE>
 __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t nbytes, const uint64_t* st64,
@@ -70,7 +71,43 @@ __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t
       if ((MODE & kCheck) && s != (uint32_t)st64[r]) atomicAdd(c.sink + 1, 1u);
     }
   };
+  __shared__ __attribute__((aligned(16))) uint32_t stage[8][1024 + 32];  // 4 KiB + slack per wave
+  // kTabLds: 32 KiB more LDS per workgroup (k_tpl_lane's CRC position tables): 2 workgroups per CU
+  constexpr uint32_t kPad = (MODE & kTabLds) ? ((MODE & kTab8) ? 2048u : 8192u) : 1u;
+  __shared__ uint32_t tabpad[kPad];
+  if (MODE & kTabLds) {
+    for (uint32_t i = threadIdx.x; i < kPad; i += 512u) tabpad[i] = i;
+    __syncthreads();
+  }
+  uint32_t* st_w = stage[threadIdx.x >> 6];
   auto window = [&](uint32_t e, uint32_t (&w)[16]) {
+    if (MODE & kStaged) {
+      // the wave's 64 records are one span: coalesced 16-byte loads of it into LDS, then each lane
+      // reads its window from LDS (aligned dwords + alignbyte)
+      const uint32_t e_last = __builtin_amdgcn_readlane(e, 63), e_first = __builtin_amdgcn_readfirstlane(e);
+      const uint32_t lo = (e_first >= 64u ? e_first - 64u : 0u) & ~15u;
+      const uint32_t hi = e_last;
+      for (uint32_t k = 0; k < 4u; ++k) {
+        const uint32_t off = lo + 16u * (lane + 64u * k);
+        if (off < hi) {
+          const u32x4 v = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          *reinterpret_cast<u32x4*>(st_w + 4u * (lane + 64u * k)) = v;
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // (lgkmcnt(0): the wave's LDS writes done)
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t b0 = e >= 64u ? e - 64u - lo : 0u;
+      const uint32_t q0 = b0 >> 2, sh = b0 & 3u;
+      uint32_t prev = st_w[q0];
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const uint32_t nx = st_w[q0 + i + 1];
+        w[i] = __builtin_amdgcn_alignbyte(nx, prev, sh);
+        prev = nx;
+      }
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
     const uint32_t voff = e >= 64u ? e - 64u : 0xffffff00u;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -86,13 +123,18 @@ __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t
     uint32_t x = 0;
 #pragma unroll
     for (int i = 0; i < 16; ++i) x ^= w[i] * (uint32_t)(2 * i + 1);
+    if (MODE & kTabLds) x ^= tabpad[x & (kPad - 1u)];
     acc += x;
     if (MODE & kStore) {
       if (r < n) {
-        c.status[r] = (int32_t)((x & 1u) & (e - s == 0u));  // 0 in practice
-        c.verdict[r] = 7;
-        c.ord0[r] = 1;
-        c.ord1[r] = 2;
+        if (!(MODE & kNoSV)) {
+          c.status[r] = (int32_t)((x & 1u) & (e - s == 0u));  // 0 in practice
+          c.verdict[r] = 7;
+        }
+        if (!(MODE & kNoOrd)) {
+          c.ord0[r] = 1;
+          c.ord1[r] = 2;
+        }
         c.v[r] = w[10] & 0x7fu;
         c.boff[r] = e - 16u;
         c.blen[r] = 12u;
@@ -199,22 +241,23 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(bad, c.sink, 8, hipMemcpyDeviceToHost));
   printf("{\"dpp_wave_shr_check_mismatches\": %u}\n", bad[1]);
   printf("{\"records\": %u, \"bytes\": %u}\n", n, nb);
-  auto rep = [&](const char* name, int mode, uint32_t tpw, float ms) {
+  auto rep_ = [&](const char* name, int mode, uint32_t tpw, float ms) {
     const double rd = (double)nb + (mode & kU64 ? 16.0 : 4.0) * n;
-    const double wr = mode & kStore ? 25.0 * n : 0.0;
+    const double wr = mode & kStore ? (25.0 - (mode & kNoSV ? 5.0 : 0.0) - (mode & kNoOrd ? 4.0 : 0.0)) * n : 0.0;
     printf("{\"variant\": \"%s\", \"tiles_per_wave\": %u, \"ms\": %.4f, \"alg_TBps\": %.3f, \"frac\": %.4f, "
            "\"framed_GiBps\": %.1f}\n",
            name, tpw, ms, (rd + wr) / ms / 1e9, (rd + wr) / ms / 1e9 / 8.0, nb / (ms / 1e3) / 1073741824.0);
     fflush(stdout);
   };
-  for (uint32_t tpw : {1u, 2u, 4u}) {
-    rep("read_u64", kU64, tpw, run<kU64>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-    rep("read_u32", 0, tpw, run<0>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-    rep("rw_u64", kU64 | kStore, tpw, run<kU64 | kStore>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-    rep("rw_u32", kStore, tpw, run<kStore>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-    rep("rw_u64_pipe", kU64 | kStore | kPipe, tpw,
-        run<kU64 | kStore | kPipe>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-    rep("rw_u32_pipe", kStore | kPipe, tpw, run<kStore | kPipe>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
-  }
+  for (int rep = 0; rep < 2; ++rep)
+    for (uint32_t tpw : {1u}) {
+      rep_("rw_u32_tab", kStore | kTabLds, tpw, run<kStore | kTabLds>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("rw_u32_staged_tab8", kStore | kStaged | kTabLds | kTab8, tpw,
+           run<kStore | kStaged | kTabLds | kTab8>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("rw_u32_values_only_staged_tab8", kStore | kNoSV | kNoOrd | kStaged | kTabLds | kTab8, tpw,
+           run<kStore | kNoSV | kNoOrd | kStaged | kTabLds | kTab8>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("rw_u32_noord_staged_tab8", kStore | kNoOrd | kStaged | kTabLds | kTab8, tpw,
+           run<kStore | kNoOrd | kStaged | kTabLds | kTab8>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+    }
   return 0;
 }

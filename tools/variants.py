@@ -13,6 +13,8 @@ REPO = Path(__file__).resolve().parents[1]
 CS = REPO / "tfrecords-reader_amd" / "csrc"
 
 VARIANTS = {
+    # k_tpl_lane printing every record it leaves to k_lane_count (debug)
+    "dbgtpl": [("tfrg_tpl.hip", "#include <hip/hip_runtime.h>", "#define TFRG_DEBUG_TPL 1\n#include <hip/hip_runtime.h>")],
     # k_tpl_lane: one tile (4 groups) per wave on large batches instead of two
     "t1": [("tfrg_tpl.hip", "a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;",
             "a2.gpw = need < (uint32_t)num_cus ? 2u : 4u;"),
