@@ -297,7 +297,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     wall = time.perf_counter() - t0
     if ctx.dist:
         tdist.barrier()
-    elapsed = max(wall, e0.elapsed_time(e1) / 1e3)
+    ev_s = e0.elapsed_time(e1) / 1e3
+    elapsed = max(wall, ev_s)
     if ctx.dist:
         cdev = dev if ctx.backend == "nccl" else torch.device("cpu")
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
@@ -306,6 +307,10 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     infos = sd.infos(plan)
     _check(infos)
     dev_bytes, reruns = sd.device_bytes()
+    # every timed decode was complete as launched: none re-run (a value hint too small, or an
+    # optimistic decode that left records; the steps decode the same input, so the confirmation of
+    # the last one stands for all of them)
+    assert reruns == 0, f"{reruns} decodes re-run after the timed region"
 
     # ---- per-kernel durations: HIP events recorded by libtfrg on the launch stream, the batches
     # run back to back on one stream so that no launch overlaps another batch's
@@ -380,9 +385,14 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         # device memory of the decode contexts (value columns sized from the learning sample), and
         # of the resident input, in multiples of the input
         "device_memory": {"contexts_bytes": dev_bytes, "x_input": round(dev_bytes / max(nbytes, 1), 3),
-                          "worst_case_reruns": reruns},
+                          "reruns": reruns},
+        # optimistic decodes (k_tpl_lane + k_quiet_finish alone, confirmed by tfrg_result_info)
+        "optimistic": os.environ.get("TFRG_OPTIMISTIC", "1") != "0",
         "streams": len(handles),
         "ms_per_step": round(ms_step, 4),
+        # (the step is the larger of the host's wall clock and the GPU events: a small batch's step
+        # can be the host's enqueue rate)
+        "step_parts_ms": {"host_wall": round(wall / steps * 1e3, 4), "gpu_events": round(ev_s / steps * 1e3, 4)},
         "GiB_s": round(framed / (ms_step / 1e3) / 2**30, 3),
         "examples_per_s": round(n / (ms_step / 1e3), 1),
         "kernels_ms": {k: round(v, 4) for k, v in kern_ms.items()},

@@ -119,7 +119,8 @@ int tfrg_ctx_set_record_bound(tfrg_ctx* ctx, uint64_t max_record_bytes);
  * values exceed a hint is re-run with the worst case inside tfrg_result_info before it returns (the
  * results are always complete); tfrg_ctx_device_bytes counts those re-runs. */
 int tfrg_ctx_set_value_caps(tfrg_ctx* ctx, uint64_t int64_values, uint64_t float_values, uint64_t bytes_values);
-/* device memory held by the context (bytes) and the decodes re-run because a hint was too small */
+/* device memory held by the context (bytes) and the decodes re-run so far: a value-capacity hint was
+ * too small, or an optimistic decode left records (tfrg_result_info) */
 int tfrg_ctx_device_bytes(tfrg_ctx* ctx, uint64_t* bytes, uint64_t* hint_reruns);
 /* wavefront records spanning <= nbytes are staged in LDS (clamped to the kernel's 12 KiB stage;
  * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
@@ -232,7 +233,13 @@ typedef struct tfrg_info {
   uint64_t placed_slots;
 } tfrg_info;
 
-/* Waits for the last decode and returns its summary. */
+/* Waits for the last decode and returns its summary. Optimistic decodes: when the context's record
+ * shapes took their whole learning sample, every slot is a single value and no record can exceed
+ * lane_max (tfrg_ctx_set_record_bound), a decode is launched as the template pass alone plus one
+ * bookkeeping kernel; this call confirms that every record took a shape, or re-runs the same decode
+ * with every pass before it returns (its inputs must still be in place: the decode is not complete
+ * before this call, tfrg_result_fetch or tfrg_result_device). Env TFRG_OPTIMISTIC=0 at context
+ * creation turns it off. */
 int tfrg_result_info(tfrg_ctx* ctx, tfrg_info* info);
 
 /* Columnar result. Per record: status/aux/verdict. Per slot s (row-major [n_slots][n]):
@@ -260,7 +267,8 @@ typedef struct tfrg_columns {
 
 /* device pointers of the last result (valid until the next decode / destroy). Asynchronous: the
  * columns are complete once the decode's stream reaches this call (it enqueues the identity row
- * splits of the placed slots there, once per decode). */
+ * splits of the placed slots there, once per decode). After an optimistic decode (tfrg_result_info)
+ * it first synchronizes the decode's stream to confirm it, re-running it in full if needed. */
 int tfrg_result_device(tfrg_ctx* ctx, tfrg_columns* cols);
 /* copy the last result into caller host buffers sized from tfrg_info; NULL members are skipped */
 int tfrg_result_fetch(tfrg_ctx* ctx, const tfrg_columns* host);

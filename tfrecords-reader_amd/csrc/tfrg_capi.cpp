@@ -147,7 +147,13 @@ struct tfrg_ctx {
   uint64_t hint_i64 = 0, hint_f32 = 0, hint_b = 0;
   bool hinted = false;  // the last decode ran with a hint below its worst case
   bool no_hints = false;  // (the re-run: the worst case)
-  uint64_t hint_reruns = 0;  // decodes re-run because a hint was too small
+  uint64_t hint_reruns = 0;  // decodes re-run: a hint was too small, or an optimistic decode incomplete
+  // optimistic decodes (launch_all): a batch of C1-shaped records whose templates took the learning
+  // sample is launched as k_tpl_lane + k_quiet_finish; the decode is complete once tfrg_result_info
+  // (or tfrg_result_device) has read that no record was left, else it is re-run with every pass
+  bool optimistic_on = true;  // (env TFRG_OPTIMISTIC=0: off, for A/B measurements)
+  bool no_quiet = false;      // (the re-run)
+  bool opt_pending = false;   // the last decode ran optimistically and is not confirmed yet
   struct LastCall {
     const uint8_t* d_bytes;
     uint64_t nbytes;
@@ -176,6 +182,7 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
+  if (const char* e = getenv("TFRG_OPTIMISTIC")) c->optimistic_on = atoi(e) != 0;
   if (const char* e = getenv("TFRG_DEBUG_POISON_LOC")) {  // "r0,r1,..." (at most 4)
     char* q = const_cast<char*>(e);
     for (int i = 0; i < 4 && *q; ++i) {
@@ -1007,6 +1014,9 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   cfg.lane_max = c->lane_max;
   cfg.wave_stage = c->wave_stage;
   memcpy(cfg.poison, c->poison, sizeof(cfg.poison));
+  // (the poison hook needs the gathers it tests)
+  cfg.optimistic = c->optimistic_on && !c->no_quiet && c->poison[0] == 0xffffffffu;
+  cfg.ran_optimistic = false;
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
   c->last = tfrg_ctx::LastCall{d_bytes, nbytes, cap_in, bound, n, flags, st};
@@ -1078,6 +1088,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   c->materialized = mat;
   c->have_result = true;
   c->rs_complete = false;
+  c->opt_pending = n != 0 && cfg.ran_optimistic;
   return 0;
 }
 
@@ -1115,28 +1126,44 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
                             c->in_end.as<uint64_t>(), n, flags, st);
 }
 
+// The last decode's info words and kind totals (synchronizes its stream). The same decode is re-run
+// -- its inputs are still the caller's: it has not been reported complete -- when it ran
+// optimistically and a record took no template (kInfoNeedFull: again with every pass), or when a
+// value-capacity hint was too small for it (again with the worst-case capacities).
+static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
+  bool widened = false;
+  for (;;) {
+    HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, kInfoCount * 4,
+                           hipMemcpyDeviceToHost, c->last_stream));
+    HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, 32, hipMemcpyDeviceToHost, c->last_stream));
+    HIP_TRY(hipStreamSynchronize(c->last_stream));
+    const bool full = h[kInfoNeedFull] != 0;  // (only an optimistic decode sets it)
+    const bool widen = h[kInfoOverflow] && c->hinted && !widened;
+    if (!full && !widen) break;
+    const tfrg_ctx::LastCall L = c->last;
+    c->no_quiet = true;
+    c->no_hints = widen;
+    c->cap_hint = L.cap_in;
+    c->call_bound = L.bound;
+    c->tsum_dirty = true;  // (the optimistic pass skipped the tile sums; clear every scan word)
+    const int rc = decode_device_any(c, L.d_bytes, L.nbytes, c->last_off, L.n, L.flags, L.st);
+    c->no_quiet = false;
+    c->no_hints = false;
+    if (rc) return rc;
+    widened |= widen;
+    ++c->hint_reruns;
+  }
+  c->opt_pending = false;
+  return 0;
+}
+
 int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   if (!c || !c->have_result) return TFRG_E_ARG;
   HIP_TRY(hipSetDevice(c->device));
   uint32_t h[kInfoCount] = {0};
   uint64_t kt[4] = {0, 0, 0, 0};
-  for (int attempt = 0;; ++attempt) {
-    HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, sizeof(h), hipMemcpyDeviceToHost,
-                           c->last_stream));
-    HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, sizeof(kt), hipMemcpyDeviceToHost, c->last_stream));
-    HIP_TRY(hipStreamSynchronize(c->last_stream));
-    if (!h[kInfoOverflow] || !c->hinted || attempt) break;
-    // a value-capacity hint was too small for this batch: the same decode again with the worst-case
-    // capacities (its inputs are still the caller's: the decode has not been reported complete)
-    const tfrg_ctx::LastCall L = c->last;
-    c->no_hints = true;
-    c->cap_hint = L.cap_in;
-    c->call_bound = L.bound;
-    const int rc = decode_device_any(c, L.d_bytes, L.nbytes, c->last_off, L.n, L.flags, L.st);
-    c->no_hints = false;
-    if (rc) return rc;
-    ++c->hint_reruns;
-  }
+  const int rc = finish_decode(c, h, kt);
+  if (rc) return rc;
   uint64_t blen = 0;
   if (c->materialized && !h[kInfoOverflow]) {  // the byte column's length: offsets[nb]
     const uint64_t nb = c->n ? kt[TFRG_KIND_BYTES] : 0;
@@ -1166,6 +1193,13 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
 
 int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
   if (!c || !c->have_result) return TFRG_E_ARG;
+  if (c->opt_pending) {  // an optimistic decode: confirmed (or re-run in full) before the view
+    HIP_TRY(hipSetDevice(c->device));
+    uint32_t h[kInfoCount];
+    uint64_t kt[4];
+    const int rc = finish_decode(c, h, kt);
+    if (rc) return rc;
+  }
   if (!c->rs_complete && c->n_slots && c->n) {
     // a self-consistent view: the identity rows of the finally placed slots, which the decode does
     // not store, are written by one small kernel on the decode's stream (placed mask read on the

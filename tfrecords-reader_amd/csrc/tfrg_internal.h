@@ -99,7 +99,7 @@ struct LeanTgt {
 struct LeanArgs {
   uint32_t n_tpl;
   uint32_t lane_max;
-  uint32_t* tsum;  // tile sums, slot k's at k * tile_stride
+  uint32_t* tsum;  // tile sums, slot k's at k * tile_stride (nullptr: an optimistic decode, none stored)
   uint32_t n_slots;
   uint32_t tile_stride;
   uint32_t img_words;  // the templates' lane image (DevSchema::tpl_img), copied into LDS
@@ -187,8 +187,10 @@ enum InfoIdx : uint32_t {
   kInfoResid = 17,       // k_tpl_lane: 64-record groups listed for k_lane_count (records no template took)
   kInfoPlacedLo = 18,    // [18..19] k_down_gather: the (first 64) slots whose speculative placement is final
   kInfoPlacedHi = 19,
-  kInfoCount = 20
+  kInfoNeedFull = 20,    // k_quiet_finish: an optimistic decode found records no template took (re-run in full)
+  kInfoCount = 22        // (even: the two slots' kInfoCrcCtr words are 8-byte aligned u64 atomics)
 };
+static_assert(kInfoCount % 2 == 0 && kInfoCrcCtr % 2 == 0, "u64 info words stay 8-byte aligned in both slots");
 
 // Deferred packed int64 bodies of records walked from HBM (k_lane_count -> k_body_count): a wave
 // reserves one block of 64 rows, row = one record, kDeferK entries (record, slot, absolute body
@@ -299,6 +301,9 @@ struct LaunchCfg {
   bool body_count;         // deferred packed bodies possible (DevOut::dq): launch k_body_count
   uint32_t poison[4];      // debug hook (env TFRG_DEBUG_POISON_LOC): records whose list locations are
                            // overwritten after the count passes (0xffffffff: none)
+  bool optimistic;         // allow an optimistic decode (launch_all: k_tpl_lane + k_quiet_finish only)
+  bool ran_optimistic;     // (out) this decode was launched optimistically: it is complete only once
+                           // the host has read kInfoNeedFull as 0 (else it is re-run in full)
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).
@@ -311,7 +316,7 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
                            const uint32_t* d_tab, int num_cus, hipStream_t st);
 hipError_t launch_fill_placed_rows(uint32_t* rs, const uint32_t* info, uint32_t n_slots, uint32_t n, hipStream_t st);
 hipError_t launch_stream_read(const void* d, uint64_t nbytes, uint32_t* sink, hipStream_t st, int variant);
-hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, const LaunchCfg& cfg,
+hipError_t launch_decode(const DevBatch& b, const DevSchema& sc, const DevOut& o, LaunchCfg& cfg,
                          const uint32_t* d_crc_tables, const uint32_t* d_wave_consts, hipStream_t stream,
                          hipEvent_t* ev);
 

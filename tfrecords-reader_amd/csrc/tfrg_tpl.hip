@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   };
   auto flush = [&](uint32_t g) {  // the tile sums of group g's tile: the first writer of tsum (zero
     // before the decode; k_lane_count's residual records add theirs with atomics after this kernel)
-    if (lane < A.n_slots && acc) {
+    if (lane < A.n_slots && acc && A.tsum) {
       if (whole)
         A.tsum[lane * A.tile_stride + (g >> 2)] = acc;
       else

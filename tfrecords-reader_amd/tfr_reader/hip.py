@@ -242,7 +242,8 @@ class HipDecoder:
                 "tfrg_ctx_set_value_caps")
 
     def device_bytes(self) -> tuple[int, int]:
-        """(device memory held by this decoder's context, decodes re-run because a hint was too small)."""
+        """(device memory held by this decoder's context, decodes re-run: a value-capacity hint too
+        small, or an optimistic decode that left records no template took)."""
         b, r = C.c_uint64(), C.c_uint64()
         N.check(self._lib.tfrg_ctx_device_bytes(self._ctx, C.byref(b), C.byref(r)), "tfrg_ctx_device_bytes")
         return int(b.value), int(r.value)

@@ -323,7 +323,8 @@ class ShardDecoder:
                                     int(firsts[k]), r1 - r0, stream=s, **kw)
 
     def device_bytes(self) -> tuple[int, int]:
-        """(device memory of every batch context, worst-case re-runs so far)."""
+        """(device memory of every batch context, decodes re-run so far: a value hint too small or
+        an optimistic decode that left records, tfrg_ctx_device_bytes)."""
         b = r = 0
         for d in self.decs:
             x, y = d.device_bytes()
