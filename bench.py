@@ -49,7 +49,7 @@ N_FILES = 256  # BASELINE.json configs[4]: the directory of 256 files
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--files", type=int, default=N_FILES, help="files in the C4 directory (partitioned over ranks)")
     # 2 GiB batches: 2,170 -> 2,229 GiB/s over 1 GiB on one box, +0.9 / +2.3 % on two others
@@ -386,7 +386,7 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         # of the resident input, in multiples of the input
         "device_memory": {"contexts_bytes": dev_bytes, "x_input": round(dev_bytes / max(nbytes, 1), 3),
                           "reruns": reruns},
-        # optimistic decodes (k_tpl_lane + k_quiet_finish alone, confirmed by tfrg_result_info)
+        # optimistic decodes (k_tpl_lane alone, confirmed by tfrg_result_info)
         "optimistic": os.environ.get("TFRG_OPTIMISTIC", "1") != "0",
         "streams": len(handles),
         "ms_per_step": round(ms_step, 4),
@@ -567,7 +567,11 @@ def run(args) -> None:
                 cw = c4_workload("c1v", 0, 8, args.files, "c4_c1v_rank0of8")
             else:
                 cw = single_workload(name)
-            m = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps)
+            # (a small batch's step is tens of microseconds: enough steps for a timed region of a few
+            # milliseconds, so the first launch after the idle synchronize does not weigh as a step)
+            c_steps = max(5, args.steps // 2, min(500, int(1e11 // max(cw.framed_bytes, 1))))
+            m = measure(ctx, cw, c_steps, max(args.warmup, min(50, c_steps // 10)), args.profile_steps)
+            m["steps"] = c_steps
             del m["_d_bytes"], m["_elapsed"]
             if name == "c4of8":  # the same share without record-shape templates (canonical walk only)
                 t = measure(ctx, cw, max(5, args.steps // 2), args.warmup, args.profile_steps, templates=False)

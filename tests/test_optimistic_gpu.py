@@ -1,5 +1,5 @@
 """Optimistic decodes: a batch of a schema whose record shapes took the whole learning sample, every
-slot a single value (C1-shaped), is launched as k_tpl_lane + k_quiet_finish alone. When a record of
+slot a single value (C1-shaped), is launched as k_tpl_lane alone (its last workgroup finishes the decode). When a record of
 the batch takes no template, the decode is re-run with every pass before any result is read
 (tfrg_result_info, or tfrg_result_device without it). Results must equal the decode with every
 pass (TFRG_OPTIMISTIC=0) column by column, and the oracle record by record."""

@@ -149,7 +149,7 @@ struct tfrg_ctx {
   bool no_hints = false;  // (the re-run: the worst case)
   uint64_t hint_reruns = 0;  // decodes re-run: a hint was too small, or an optimistic decode incomplete
   // optimistic decodes (launch_all): a batch of C1-shaped records whose templates took the learning
-  // sample is launched as k_tpl_lane + k_quiet_finish; the decode is complete once tfrg_result_info
+  // sample is launched as k_tpl_lane alone (its last workgroup finishes it); the decode is complete once tfrg_result_info
   // (or tfrg_result_device) has read that no record was left, else it is re-run with every pass
   bool optimistic_on = true;  // (env TFRG_OPTIMISTIC=0: off, for A/B measurements)
   bool no_quiet = false;      // (the re-run)
@@ -1128,7 +1128,7 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
 
 // The last decode's info words and kind totals (synchronizes its stream). The same decode is re-run
 // -- its inputs are still the caller's: it has not been reported complete -- when it ran
-// optimistically and a record took no template (kInfoNeedFull: again with every pass), or when a
+// optimistically and a record took no template (kInfoResid: again with every pass), or when a
 // value-capacity hint was too small for it (again with the worst-case capacities).
 static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
   bool widened = false;
@@ -1137,7 +1137,7 @@ static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
                            hipMemcpyDeviceToHost, c->last_stream));
     HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, 32, hipMemcpyDeviceToHost, c->last_stream));
     HIP_TRY(hipStreamSynchronize(c->last_stream));
-    const bool full = h[kInfoNeedFull] != 0;  // (only an optimistic decode sets it)
+    const bool full = c->opt_pending && h[kInfoResid] != 0;  // (records no template took)
     const bool widen = h[kInfoOverflow] && c->hinted && !widened;
     if (!full && !widen) break;
     const tfrg_ctx::LastCall L = c->last;

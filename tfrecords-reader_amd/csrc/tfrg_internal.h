@@ -103,10 +103,12 @@ struct LeanArgs {
   uint32_t n_slots;
   uint32_t tile_stride;
   uint32_t img_words;  // the templates' lane image (DevSchema::tpl_img), copied into LDS
-  uint32_t gpw;    // (launch_tpl_lane) 64-record groups per wave: 2 (half a tile: small batches,
+  uint32_t gpw;    // (launch_tpl_lane) 64-record groups per wave: 1 or 2 (part of a tile: small batches,
                    // twice the waves, tile sums added atomically) or a multiple of 4 (whole tiles)
   uint32_t bsplit; // workgroups from this one on take 2 groups per wave, from group gsplit on (the
   uint32_t gsplit; // batch's tail in small pieces: the last workgroups dispatched finish together)
+  const uint8_t* finish;  // optimistic decode: DevSchema::slot_kind, and the last workgroup finishes
+                          // the decode (tpl_quiet_finish); nullptr: the passes after this kernel do
   LeanTgt tg[kLeanMaxSlots];
 };
 
@@ -187,10 +189,12 @@ enum InfoIdx : uint32_t {
   kInfoResid = 17,       // k_tpl_lane: 64-record groups listed for k_lane_count (records no template took)
   kInfoPlacedLo = 18,    // [18..19] k_down_gather: the (first 64) slots whose speculative placement is final
   kInfoPlacedHi = 19,
-  kInfoNeedFull = 20,    // k_quiet_finish: an optimistic decode found records no template took (re-run in full)
-  kInfoCount = 22        // (even: the two slots' kInfoCrcCtr words are 8-byte aligned u64 atomics)
+  kInfoTplDone = 20,     // [20..21] u64, optimistic decodes: k_tpl_lane workgroups finished | groups
+                         // they listed << 32 (one atomic: the last workgroup knows the total)
+  kInfoCount = 22        // (even: the two slots' u64 words stay 8-byte aligned)
 };
-static_assert(kInfoCount % 2 == 0 && kInfoCrcCtr % 2 == 0, "u64 info words stay 8-byte aligned in both slots");
+static_assert(kInfoCount % 2 == 0 && kInfoCrcCtr % 2 == 0 && kInfoTplDone % 2 == 0,
+              "u64 info words stay 8-byte aligned in both slots");
 
 // Deferred packed int64 bodies of records walked from HBM (k_lane_count -> k_body_count): a wave
 // reserves one block of 64 rows, row = one record, kDeferK entries (record, slot, absolute body
@@ -301,7 +305,7 @@ struct LaunchCfg {
   bool body_count;         // deferred packed bodies possible (DevOut::dq): launch k_body_count
   uint32_t poison[4];      // debug hook (env TFRG_DEBUG_POISON_LOC): records whose list locations are
                            // overwritten after the count passes (0xffffffff: none)
-  bool optimistic;         // allow an optimistic decode (launch_all: k_tpl_lane + k_quiet_finish only)
+  bool optimistic;         // allow an optimistic decode (launch_all: k_tpl_lane alone)
   bool ran_optimistic;     // (out) this decode was launched optimistically: it is complete only once
                            // the host has read kInfoNeedFull as 0 (else it is re-run in full)
 };

@@ -3397,39 +3397,6 @@ __global__ void k_poison_loc(DevOut o, uint32_t n, uint32_t n_slots, uint4 recs)
 
 // ------------------------------------------------------------------------------------------------
 // launcher
-// The end of an optimistic decode (launch_all): k_tpl_lane took every record -- no group listed --
-// so every slot's placement is final and the passes after it would have nothing to do but their
-// bookkeeping, done here by one workgroup: the next decode's info words zeroed (k_lane_count), slot
-// totals n, column bases and kind totals (k_spine's every-slot-placed path), the last row split of
-// every slot and the placed mask (k_down_gather). A group listed (a record no template took, or one
-// that failed): kInfoNeedFull, and the host re-runs the decode with every pass (tfrg_result_info).
-__global__ __launch_bounds__(256) void k_quiet_finish(DevOut o, const uint8_t* __restrict__ slot_kind, uint32_t n_slots,
-                                                      uint32_t n) {
-  if (threadIdx.x < kInfoCount) o.info_next[threadIdx.x] = 0u;
-  if (o.info[kInfoResid] != 0u) {  // (uniform)
-    if (threadIdx.x == 0) o.info[kInfoNeedFull] = 1u;
-    return;
-  }
-  for (uint32_t k = threadIdx.x; k < n_slots; k += 256u) {
-    o.totals[k] = n;
-    o.rs[(size_t)k * (n + 1u) + n] = n;
-  }
-  if (threadIdx.x == 0) {
-    uint64_t acc[4] = {0, 0, 0, 0};
-    for (uint32_t k = 0; k < n_slots; ++k) {
-      const uint32_t kd = slot_kind[k] & 3u;
-      o.slot_base[k] = acc[kd];
-      acc[kd] += n;
-    }
-    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
-    if (acc[TFRG_KIND_INT64] > o.cap_i64 || acc[TFRG_KIND_FLOAT] > o.cap_f32 || acc[TFRG_KIND_BYTES] > o.cap_b)
-      o.info[kInfoOverflow] = 1u;
-    const uint64_t pm = n_slots >= 64u ? ~0ull : (1ull << n_slots) - 1ull;
-    o.info[kInfoPlacedLo] = (uint32_t)pm;
-    o.info[kInfoPlacedHi] = (uint32_t)(pm >> 32);
-  }
-}
-
 // ------------------------------------------------------------------------------------------------
 constexpr int kLaneRep = 1;  // CRC table bank replication in the lane kernel (slice-by-8: 8 KiB per copy)
 
@@ -3474,9 +3441,10 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   bool all_spec = scx.spec && cfg.spec_h && S <= 64;
   for (size_t k = 0; all_spec && k < S; ++k) all_spec = cfg.spec_h[k] != 0u;
   // Optimistic: quiet with every slot placed (C1-shaped batches). A batch all of whose records take a
-  // template is complete after k_tpl_lane; the passes after it would only launch. k_quiet_finish does
-  // their bookkeeping, or flags the batch for a full re-run by the host (tfrg_result_info) if any
-  // record did not take a template. Saves five dependent launches (~4 us each) per batch.
+  // template is complete after k_tpl_lane; the passes after it would only launch. The last
+  // workgroup of k_tpl_lane does their bookkeeping (tpl_quiet_finish), or flags the batch for a full
+  // re-run by the host (tfrg_result_info) if a record took no template. Saves five dependent
+  // launches (~4 us each) per batch.
   cfg.ran_optimistic = cfg.optimistic && quiet && all_spec && S > 0;
   DevOut ox = o;
   if (!lean) {
@@ -3490,6 +3458,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     a.img_words = sc.tpl_img_words;
     a.lane_max = cfg.lane_max;
     a.tsum = cfg.ran_optimistic ? nullptr : o.tsum;  // (placed slots: no scan; a re-run clears tsum)
+    a.finish = cfg.ran_optimistic ? sc.slot_kind : nullptr;
     a.n_slots = (uint32_t)S;
     a.tile_stride = o.tile_stride;
     const uint64_t n = b.n;
@@ -3515,10 +3484,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     const hipError_t e = launch_tpl_lane(b, ox, a, sc.tpl_img, sc.tpl_w, d_tab, cfg.num_cus, st);
     if (e != hipSuccess) return e;
   }
-  if (cfg.ran_optimistic) {
-    mark(kStageLaneCount);
-    hipLaunchKernelGGL(k_quiet_finish, dim3(1), dim3(256), 0, st, ox, sc.slot_kind, (uint32_t)S, b.n);
-    for (int i = kStageBodyCount; i <= kStageMaterialize; ++i) mark(i);
+  if (cfg.ran_optimistic) {  // (k_tpl_lane's last workgroup finished the decode)
+    for (int i = kStageLaneCount; i <= kStageMaterialize; ++i) mark(i);
     return hipGetLastError();
   }
   mark(kStageLaneCount);

@@ -100,6 +100,39 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
   return x;
 }
 
+// The end of an optimistic decode (launch_all), by the last workgroup of k_tpl_lane: no 64-record
+// group was listed -- every record took a template -- so every slot's placement is final and the
+// passes after k_tpl_lane would have nothing to do but their bookkeeping, done here: the next
+// decode's info words zeroed (k_lane_count), slot totals n, column bases and kind totals (k_spine's
+// every-slot-placed path), the last row split of every slot and the placed mask (k_down_gather). A
+// group listed (a record no template took, or one that failed): kInfoNeedFull, and the host re-runs
+// the decode with every pass (tfrg_result_info). Saves the five dependent launches after it.
+// `listed`: the groups every workgroup listed, from the same atomic as the workgroup tickets (no
+// fence: a release per workgroup would write back the XCD's L2 every time).
+__device__ void tpl_quiet_finish(const DevOut& o, const uint8_t* slot_kind, uint32_t n_slots, uint32_t n,
+                                 uint32_t listed) {
+  if (threadIdx.x < kInfoCount) o.info_next[threadIdx.x] = 0u;
+  if (listed != 0u) return;  // (uniform; the host sees kInfoResid and re-runs the decode)
+  for (uint32_t k = threadIdx.x; k < n_slots; k += kTplBlock) {
+    o.totals[k] = n;
+    o.rs[(size_t)k * (n + 1u) + n] = n;
+  }
+  if (threadIdx.x == 0) {
+    uint64_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < n_slots; ++k) {
+      const uint32_t kd = slot_kind[k] & 3u;
+      o.slot_base[k] = acc[kd];
+      acc[kd] += n;
+    }
+    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+    if (acc[TFRG_KIND_INT64] > o.cap_i64 || acc[TFRG_KIND_FLOAT] > o.cap_f32 || acc[TFRG_KIND_BYTES] > o.cap_b)
+      o.info[kInfoOverflow] = 1u;
+    const uint64_t pm = n_slots >= 64u ? ~0ull : (1ull << n_slots) - 1ull;
+    o.info[kInfoPlacedLo] = (uint32_t)pm;
+    o.info[kInfoPlacedHi] = (uint32_t)(pm >> 32);
+  }
+}
+
 template <int W, int OM>
 __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_tpl_lane(
     DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ img, const uint32_t* __restrict__ tabs) {
@@ -126,8 +159,9 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   // tile (gpw 2: small batches on twice the waves, tile sums added atomically)
   const bool tail = blockIdx.x >= A.bsplit;
   const uint32_t gpw = tail ? 2u : A.gpw;
-  const uint32_t gbeg = tail ? A.gsplit + ((blockIdx.x - A.bsplit) * kWaves + wib) * 2u : (blockIdx.x * kWaves + wib) * gpw;
-  if (gbeg >= ngroups) return;  // (wave-uniform; no barrier follows)
+  const uint32_t gbeg0 = tail ? A.gsplit + ((blockIdx.x - A.bsplit) * kWaves + wib) * 2u : (blockIdx.x * kWaves + wib) * gpw;
+  // (a wave past the batch runs no group: gend = gbeg; it still reaches the optimistic epilogue)
+  const uint32_t gbeg = gbeg0 < ngroups ? gbeg0 : ngroups;
   const uint32_t gend = gbeg + gpw < ngroups ? gbeg + gpw : ngroups;
   const bool whole = (gpw & 3u) == 0u;
 
@@ -200,6 +234,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
   };
   uint32_t acc = 0;  // lane k: slot k's value count over this tile's records so far
+  uint32_t listed = 0;  // (wave-uniform) groups this wave listed for k_lane_count
   // one group: every lane matches the template its payload length selects (kLiLut; the next one of
   // the same length if that fails), then the dict into the columns, one store per column
   auto proc = [&](const wvec& w, uint32_t g, const LaneOff& f) {
@@ -303,6 +338,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       o.lmask[g] = mm;
       if (mm) o.rlist[atomicAdd(&o.info[kInfoResid], 1u)] = g;
     }
+    listed += mm ? 1u : 0u;
   };
   auto flush = [&](uint32_t g) {  // the tile sums of group g's tile: the first writer of tsum (zero
     // before the decode; k_lane_count's residual records add theirs with atomics after this kernel)
@@ -346,6 +382,22 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);
   }
 #endif
+  if (A.finish) {  // (uniform) optimistic decode: the last workgroup to finish ends it
+    __shared__ uint32_t s_listed[kWaves];
+    __shared__ uint32_t s_last, s_total;
+    if (lane == 0) s_listed[wib] = listed;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t mine = 0;
+      for (uint32_t i = 0; i < kWaves; ++i) mine += s_listed[i];
+      const uint64_t old = atomicAdd(reinterpret_cast<unsigned long long*>(o.info + kInfoTplDone),
+                                     ((unsigned long long)mine << 32) | 1ull);
+      s_last = (uint32_t)old == gridDim.x - 1u;
+      s_total = (uint32_t)(old >> 32) + mine;
+    }
+    __syncthreads();
+    if (s_last) tpl_quiet_finish(o, A.finish, A.n_slots, B.n, s_total);
+  }
 }
 
 }  // namespace
@@ -356,12 +408,13 @@ hipError_t launch_tpl_lane(const DevBatch& b, const DevOut& o, const LeanArgs& a
   const uint32_t tiles = (groups + 3u) / 4u;  // (one wave per 256-record tile)
   const uint32_t need = (tiles + kTplBlock / 64 - 1) / (kTplBlock / 64);
   // two tiles per wave (one for batches of fewer than 8 workgroups per CU, half a tile for batches of
-  // fewer workgroups than CUs), no resident-grid stride: workgroups retire all through the launch,
+  // fewer workgroups than CUs, a quarter -- one group -- below half as many: a latency-bound launch
+  // of a few MiB, c1file 15.5 -> 12.2 us), no resident-grid stride: workgroups retire all through the launch,
   // so the end of the batch does not wait on the waves that drew an extra round of tiles (c4of8:
   // 0.414 ms against 0.430 ms for one round of resident workgroups; the 32 KiB table copy per
   // workgroup is L2 traffic)
   LeanArgs a2 = a;
-  a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;
+  a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;
   // The dispatcher hands out workgroups in index order as slots free up, so the last ones decide
   // when the batch ends: the groups of about one round of resident workgroups (3 per CU) at the end
   // of a large batch go to workgroups of 2 groups per wave instead of gpw, and the last round idles
