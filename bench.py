@@ -313,11 +313,17 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     assert reruns == 0, f"{reruns} decodes re-run after the timed region"
 
     # ---- per-kernel durations: HIP events recorded by libtfrg on the launch stream, the batches
-    # run back to back on one stream so that no launch overlaps another batch's
-    for d in sd.decs:
-        d.set_profiling(True)
+    # run back to back on one stream so that no launch overlaps another batch's. Each profiled step
+    # follows an unprofiled one on the same stream: the GPU is busy when its first kernel starts (a
+    # step launched on an idle GPU after the host read the previous profile took ~0.1 ms longer in
+    # its first stage)
     per: dict[str, list[float]] = {}
     for _ in range(prof_steps):
+        for d in sd.decs:
+            d.set_profiling(False)
+        step([main.cuda_stream])
+        for d in sd.decs:
+            d.set_profiling(True)
         step([main.cuda_stream])
         tot: dict[str, float] = {}
         for d in sd.decs[: len(plan)]:

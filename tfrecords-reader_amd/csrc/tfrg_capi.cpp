@@ -1176,7 +1176,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->first_error = ~h[kInfoFirstError];  // (stored inverted by atomicMax; 0 = no error -> 0xffffffff)
   info->n_miss_records = h[kInfoMissRecords];
   info->n_miss_entries = h[kInfoMissEntries];
-  info->n_big = h[kInfoBig] + h[kInfoHuge];
+  info->n_big = h[kInfoBigRecs];
   info->scan_timeout = h[kInfoScanTimeout];
   for (int k = 0; k < 4; ++k) info->kind_totals[k] = kt[k];
   info->nbytes = c->nbytes;

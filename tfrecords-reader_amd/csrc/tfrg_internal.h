@@ -191,7 +191,9 @@ enum InfoIdx : uint32_t {
   kInfoPlacedHi = 19,
   kInfoTplDone = 20,     // [20..21] u64, optimistic decodes: k_tpl_lane workgroups finished | groups
                          // they listed << 32 (one atomic: the last workgroup knows the total)
-  kInfoCount = 22        // (even: the two slots' u64 words stay 8-byte aligned)
+  kInfoBigRecs = 22,     // records above lane_max (tfrg_info.n_big; kInfoBig + kInfoHuge count the
+                         // ones listed for the wave gathers: those with out-of-line lists)
+  kInfoCount = 24        // (even: the two slots' u64 words stay 8-byte aligned)
 };
 static_assert(kInfoCount % 2 == 0 && kInfoCrcCtr % 2 == 0 && kInfoTplDone % 2 == 0,
               "u64 info words stay 8-byte aligned in both slots");

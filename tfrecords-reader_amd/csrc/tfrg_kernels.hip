@@ -1442,20 +1442,15 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
       nen = rec_end(B, (uint32_t)(base + lane));
     }
     RecView v{};
-    bool mine = false;
+    bool mine = false, big = false;
     if (valid) {
       v = rec_view_se(B, cst0, cen0);
-      const bool big = v.status == TFRG_OK && v.e - v.st > lane_max;
-      if (big) {  // large record: wavefront kernels (staged ones from the front, huge from the back)
-        if (v.e - (v.st & ~15ull) <= wave_stage) {
-          const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
-          o.big_list[i] = r;
-        } else {
-          const uint32_t i = atomicAdd(&o.info[kInfoHuge], 1u);
-          o.big_list[B.n - 1u - i] = r;
-        }
-      }
+      big = v.status == TFRG_OK && v.e - v.st > lane_max;  // (listed for the wave gathers below)
       mine = !big;
+    }
+    {
+      const uint64_t bm = __ballot(big);
+      if (bm && lane == 0) atomicAdd(&o.info[kInfoBigRecs], (uint32_t)__popcll(bm));
     }
     // wave-uniform staging decision over the span of this wave's records
     const bool span_rec = fast_ok && mine && v.status == TFRG_OK;
@@ -1488,6 +1483,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     }();
     bool done = false;
     bool tried = false;
+    uint32_t nd = 0;  // packed int64 bodies of this record deferred to k_body_count
     if (staged && span_rec) {
       const FastSrc fs{stage, (uint32_t)(v.p0 - lo16), (uint32_t)v.L, v.p0};
       frame_verdicts<R, true>(B, v, T, stage, lo16, true);
@@ -1514,7 +1510,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
         blk = rfl32((uint32_t)__shfl((int)blk, 0, 64));
         if (blk >= o.dq_blocks) blk = ~0u;
       }
-      uint32_t nd = 0;
       if (bigw) {
         // (the payload CRC of a large record is role 2's stream, unless it is shorter than one round)
         const bool crc_here = mine || (uint64_t)v.L < kCrcListMin;
@@ -1568,10 +1563,12 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
         }
       }
     }
+    bool ool = MODE == 1;  // the record has an out-of-line list (MODE 1: not tracked, assumed)
     if constexpr (MODE != 1) {
       for (uint32_t k = 0; k < S; ++k) {
         const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * sink.ostride] : 0u;
         const uint32_t c = ov ? sink.count_of(k) : 0u;
+        ool |= c != 0u && !(c & kCountInline);
         if (done) {
           const size_t at = (size_t)k * B.n + r;
           o.order[at] = (uint16_t)ov;
@@ -1593,6 +1590,18 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
       }
     }
     crc_list_append(o, r, crc_j, lane);
+    // a large record goes to the wave gathers (staged ones from the front of big_list, huge ones
+    // from the back) if it has a list k_down_gather does not write: out-of-line or deferred lists, or
+    // any list of a record the exact walker takes (C2's single image views and labels need none)
+    if (big && (!done || ool || nd)) {
+      if (v.e - (v.st & ~15ull) <= wave_stage) {
+        const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
+        o.big_list[i] = r;
+      } else {
+        const uint32_t i = atomicAdd(&o.info[kInfoHuge], 1u);
+        o.big_list[B.n - 1u - i] = r;
+      }
+    }
     wave_lds_sync();  // the stage is rewritten by the next iteration
     PHASE_MARK(p5);
     PHASE_ADD(19, p4, p5);

@@ -94,9 +94,6 @@ VARIANTS = {
                   "  const uint64_t pmask = sc.spec ? (uint64_t)__ballot(lane < S && spec_placed(sc.spec, o, lane)) : 0ull;\n",
                   "  uint64_t pmask = 0;\n  if (sc.spec)\n    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;\n"
                   "  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)pmask);\n")],
-    # k_tpl_lane: one group per wave on small batches (fewer than one workgroup per CU) instead of two
-    "gpw1": [("tfrg_tpl.hip", "a2.gpw = need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;",
-              "a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
