@@ -356,8 +356,15 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     for i in infos:
         placed &= int(i.placed_slots)
     n_placed = bin(placed & ((1 << min(n_slots, 64)) - 1)).count("1")
+    # columns an optimistic decode left implicit in every batch (tfrg_info.implicit_cols: constant
+    # status / verdict, constant order words), never stored: not counted
+    implicit = 3
+    for i in infos:
+        implicit &= int(i.implicit_cols)
+    st_b = 0 if implicit & 1 else 5
+    ord_b = 0 if implicit & 2 else 2 * n_slots
     # (off_bytes: the record offsets as handed over -- 4 B of u32 ends, 8 B of u32 pairs, 16 B of u64)
-    lane_alg = small_bytes + n_small * (off_bytes + 5 + 2 * n_slots + 4 * (n_slots - n_placed)) + 8 * present_small
+    lane_alg = small_bytes + n_small * (off_bytes + st_b + ord_b + 4 * (n_slots - n_placed)) + 8 * present_small
     alg = {
         # template path: its records' framed bytes + offsets in; status, verdict, order per slot, a row
         # split (or count) per slot not placed, and a value / location word per present list out
@@ -377,8 +384,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     achieved = a_bytes / (kern_ms[dominant] / 1e3) / 1e9
     n_keys = len(sd.keys.keys)
     R = framed + off_bytes * n
-    # (SURVEY D2's W, less the row splits of placed slots, which are implicit: never stored)
-    W = 4 * n + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
+    # (SURVEY D2's W, less the row splits of placed slots and the implicit status, never stored)
+    W = (0 if implicit & 1 else 4 * n) + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
     ms_step = elapsed / steps * 1e3
     out = {
         "workload": w.desc,
@@ -394,6 +401,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
                           "reruns": reruns},
         # optimistic decodes (k_tpl_lane alone, confirmed by tfrg_result_info)
         "optimistic": os.environ.get("TFRG_OPTIMISTIC", "1") != "0",
+        # TFRG_IMPLICIT_* bits common to every batch: 1 status / verdict, 2 order words
+        "implicit_cols": implicit,
         "streams": len(handles),
         "ms_per_step": round(ms_step, 4),
         # (the step is the larger of the host's wall clock and the GPU events: a small batch's step

@@ -225,7 +225,13 @@ typedef struct tfrg_info {
   uint64_t nbytes;
   uint64_t bytes_data_len;  /* TFRG_FLAG_MATERIALIZE_BYTES: bytes in the byte column, else 0   */
   uint32_t tpl_groups_missed; /* 64-record groups with a record no record-shape template took */
-  uint32_t reserved;
+  /* TFRG_IMPLICIT_* bits: columns an optimistic decode (tfrg_result_info) did not store because every
+   * record of the batch took a record shape: STATUS -- every status 0 (aux unused) and every verdict
+   * TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC; ORDER -- every slot's order word is the
+   * same for every record (its key position in the shapes). tfrg_result_fetch fills them into the
+   * caller's buffers on the host (no copy), tfrg_result_device into the device columns (once per
+   * decode, on the decode's stream, before it returns the view). */
+  uint32_t implicit_cols;
   /* bit k: slot k (< 64) holds exactly one value per record, at row r of its column (final
    * speculative placement). Its row splits are the identity 0..n: the decode does not store them;
    * tfrg_result_fetch writes them into the caller's buffer, and tfrg_result_device into the device

@@ -67,4 +67,8 @@ enum tfrg_verdict {
   TFRG_V_TRUNCATED = 8u   /* range ran past the end of the buffer (clamped)        */
 };
 
+/* tfrg_info.implicit_cols (tfrg.h): columns an optimistic decode did not store */
+#define TFRG_IMPLICIT_STATUS 1u /* status 0, aux 0, verdict LEN_MATCH | LEN_CRC | DATA_CRC for every record */
+#define TFRG_IMPLICIT_ORDER 2u  /* every slot's order word the same for every record */
+
 #endif

@@ -49,11 +49,12 @@ def test_optimistic_decode_identical_and_rerun_on_a_miss(monkeypatch):
         a, b = on.decode(buf, st, en), full.decode(buf, st, en)  # (learns the shapes: the whole sample)
         _same(a, b)
         assert int(a.info.tpl_groups_missed) == 0 and on.device_bytes()[1] == 0  # optimistic, complete
+        assert int(a.info.implicit_cols) == 3 and int(b.info.implicit_cols) == 0  # status / order constant
         pl = _c1_odd(5000, 499)
         buf, st, en = synth.framed(pl)
         a, b = on.decode(buf, st, en), full.decode(buf, st, en)
         assert on.device_bytes()[1] == 1 and full.device_bytes()[1] == 0  # re-run once, in full
-        assert int(a.info.tpl_groups_missed) > 0
+        assert int(a.info.tpl_groups_missed) > 0 and int(a.info.implicit_cols) == 0  # (the full re-run's)
         _same(a, b)
         orc = O.Oracle()
         raw = buf.tobytes()
@@ -100,7 +101,8 @@ def test_device_view_confirms_an_optimistic_decode(monkeypatch):
         assert on.device_bytes()[1] == before + 1
         n, S = len(pl), len(ref.slot_key)
         got = {}
-        for name, dt, count in (("status", np.int32, n), ("row_splits", np.uint32, S * (n + 1)),
+        for name, dt, count in (("status", np.int32, n), ("verdict", np.uint8, n), ("order", np.uint16, S * n),
+                                ("row_splits", np.uint32, S * (n + 1)),
                                 ("i64", np.int64, int(ref.info.kind_totals[3])),
                                 ("bytes_len", np.uint32, int(ref.info.kind_totals[1]))):
             host = np.zeros(count, dt)
@@ -108,9 +110,29 @@ def test_device_view_confirms_an_optimistic_decode(monkeypatch):
             assert hip_rt.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(p), ctypes.c_size_t(host.nbytes), 2) == 0
             got[name] = host
         assert np.array_equal(got["status"], np.array(ref.status))
+        assert np.array_equal(got["verdict"], np.array(ref.verdict))
+        assert np.array_equal(got["order"].reshape(S, n), np.array(ref.order))
         assert np.array_equal(got["row_splits"].reshape(S, n + 1), np.array(ref.row_splits))
         assert np.array_equal(got["i64"], np.array(ref.i64))
         assert np.array_equal(got["bytes_len"], np.array(ref.bytes_len))
+        # a clean batch: the columns left implicit are filled into the device view
+        buf, st, en = synth.framed(synth.c1_payloads(7000, offset=5))
+        ref = full.decode(buf, st, en)
+        d_b = torch.zeros(buf.size + 32, dtype=torch.uint8, device=dev)
+        d_b[: buf.size].copy_(torch.from_numpy(buf))
+        d_s = torch.from_numpy(st.view(np.int64)).to(dev)
+        d_e = torch.from_numpy(en.view(np.int64)).to(dev)
+        torch.cuda.synchronize(dev)
+        on.decode_device(d_b.data_ptr(), buf.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0])
+        cols = on.device_columns()
+        assert int(on.info().implicit_cols) == 3
+        n = st.shape[0]
+        for name, dt, count, want in (("status", np.int32, n, np.array(ref.status)), ("verdict", np.uint8, n, np.array(ref.verdict)),
+                                      ("order", np.uint16, S * n, np.array(ref.order).reshape(-1))):
+            host = np.zeros(count, dt)
+            p = ctypes.cast(getattr(cols, name), ctypes.c_void_p).value
+            assert hip_rt.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(p), ctypes.c_size_t(host.nbytes), 2) == 0
+            assert np.array_equal(host, want), name
     finally:
         on.close()
         full.close()

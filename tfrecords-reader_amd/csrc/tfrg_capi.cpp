@@ -154,6 +154,9 @@ struct tfrg_ctx {
   bool optimistic_on = true;  // (env TFRG_OPTIMISTIC=0: off, for A/B measurements)
   bool no_quiet = false;      // (the re-run)
   bool opt_pending = false;   // the last decode ran optimistically and is not confirmed yet
+  bool ord_const = false;     // (Learned::ord_const) of the learned shapes
+  uint32_t last_implicit = 0; // TFRG_IMPLICIT_* columns the last decode did not store
+  bool cols_complete = false; // tfrg_result_device filled them into the device columns
   struct LastCall {
     const uint8_t* d_bytes;
     uint64_t nbytes;
@@ -565,6 +568,7 @@ struct Learned {
   uint32_t W = 0;
   bool have_spec = false;
   bool full = false;  // every sampled record took a kept template
+  bool ord_const = false;  // every slot (< kLeanMaxSlots) at one key position in every kept template
 };
 uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                       const uint64_t* h_end, uint32_t n, uint32_t flags, Learned& out) {
@@ -742,6 +746,14 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
     }
   }
   memcpy(&img[kLiLut], lut.data(), lut.size());
+  // every slot present at the same key position (order word) in every kept shape: an optimistic
+  // decode leaves the order column implicit (TFRG_IMPLICIT_ORDER)
+  out.ord_const = S > 0 && S <= kLeanMaxSlots;
+  for (uint32_t s2 = 0; out.ord_const && s2 < S; ++s2) {
+    const uint32_t r0 = w[kLtSlot + 3 * s2] >> 16;
+    out.ord_const = r0 != 0;
+    for (uint32_t k = 1; out.ord_const && k < nt; ++k) out.ord_const = (w[(size_t)k * kLtWords + kLtSlot + 3 * s2] >> 16) == r0;
+  }
   out.w = std::move(w);
   out.spec = std::move(spec);
   out.img = std::move(img);
@@ -785,6 +797,7 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   c->spec_h = spec;
   c->have_spec = have_spec;
   c->tpl_full = L.full;
+  c->ord_const = L.ord_const;
   return (int)nt;
 }
 
@@ -1017,6 +1030,8 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   // (the poison hook needs the gathers it tests)
   cfg.optimistic = c->optimistic_on && !c->no_quiet && c->poison[0] == 0xffffffffu;
   cfg.ran_optimistic = false;
+  cfg.ord_const = c->ord_const;
+  cfg.implicit = 0;
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
   c->last = tfrg_ctx::LastCall{d_bytes, nbytes, cap_in, bound, n, flags, st};
@@ -1089,6 +1104,8 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   c->have_result = true;
   c->rs_complete = false;
   c->opt_pending = n != 0 && cfg.ran_optimistic;
+  c->last_implicit = n != 0 ? cfg.implicit : 0u;
+  c->cols_complete = false;
   return 0;
 }
 
@@ -1183,6 +1200,7 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   info->bytes_data_len = blen;
   info->tpl_groups_missed = h[kInfoResid];
   info->placed_slots = ((uint64_t)h[kInfoPlacedHi] << 32) | h[kInfoPlacedLo];
+  info->implicit_cols = c->last_implicit;
   if (h[kInfoOverflow]) {
     set_error("value columns overflowed their capacity (overlapping ranges in a device batch): decode "
               "the ranges from host memory (tfrg_decode_host) or split the batch");
@@ -1209,6 +1227,20 @@ int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
                                     c->n_slots, c->n, c->last_stream));
   }
   c->rs_complete = true;
+  if (c->last_implicit && !c->cols_complete) {  // the constant columns of an optimistic decode
+    HIP_TRY(hipSetDevice(c->device));
+    const size_t n = c->n;
+    if (c->last_implicit & TFRG_IMPLICIT_STATUS) {
+      HIP_TRY(hipMemsetAsync(c->status.p, 0, n * 4, c->last_stream));
+      HIP_TRY(hipMemsetAsync(c->aux.p, 0, n * 8, c->last_stream));
+      HIP_TRY(hipMemsetAsync(c->verdict.p, (int)(TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC), n, c->last_stream));
+    }
+    if (c->last_implicit & TFRG_IMPLICIT_ORDER)
+      for (uint32_t k = 0; k < c->n_slots; ++k)
+        HIP_TRY(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(c->order.as<uint16_t>() + (size_t)k * n),
+                                  (unsigned short)(c->tpl_h[kLtSlot + 3 * k] >> 16), n, c->last_stream));
+  }
+  c->cols_complete = true;
   d->status = c->status.as<int32_t>();
   d->aux = c->aux.as<int64_t>();
   d->verdict = c->verdict.as<uint8_t>();
@@ -1235,10 +1267,21 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
     if (!dst || !bytes) return hipSuccess;
     return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st);
   };
-  HIP_TRY(cp(h->status, c->status.p, n * 4));
-  HIP_TRY(cp(h->aux, c->aux.p, n * 8));
-  HIP_TRY(cp(h->verdict, c->verdict.p, n));
-  HIP_TRY(cp(h->order, c->order.p, S * n * 2));
+  // (an optimistic decode's constant columns are written here, not copied: tfrg_info.implicit_cols)
+  if (info.implicit_cols & TFRG_IMPLICIT_STATUS) {
+    if (h->status) memset(h->status, 0, n * 4);
+    if (h->aux) memset(h->aux, 0, n * 8);
+    if (h->verdict) memset(h->verdict, TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC, n);
+  } else {
+    HIP_TRY(cp(h->status, c->status.p, n * 4));
+    HIP_TRY(cp(h->aux, c->aux.p, n * 8));
+    HIP_TRY(cp(h->verdict, c->verdict.p, n));
+  }
+  if ((info.implicit_cols & TFRG_IMPLICIT_ORDER) && h->order) {
+    for (size_t k = 0; k < S; ++k) std::fill_n(h->order + k * n, n, (uint16_t)(c->tpl_h[kLtSlot + 3 * k] >> 16));
+  } else {
+    HIP_TRY(cp(h->order, c->order.p, S * n * 2));
+  }
   // row splits: a placed slot's are the identity, never stored by the decode; they copy from a
   // device identity row (filled once per size), as fast as the stored rows and as asynchronous
   if (h->row_splits) {

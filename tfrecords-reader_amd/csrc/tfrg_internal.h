@@ -109,6 +109,8 @@ struct LeanArgs {
   uint32_t gsplit; // batch's tail in small pieces: the last workgroups dispatched finish together)
   const uint8_t* finish;  // optimistic decode: DevSchema::slot_kind, and the last workgroup finishes
                           // the decode (tpl_quiet_finish); nullptr: the passes after this kernel do
+  uint32_t implicit;      // optimistic decode, TFRG_IMPLICIT_* columns not stored for template hits
+                          // (constant: every record of a confirmed decode is one)
   LeanTgt tg[kLeanMaxSlots];
 };
 
@@ -309,7 +311,9 @@ struct LaunchCfg {
                            // overwritten after the count passes (0xffffffff: none)
   bool optimistic;         // allow an optimistic decode (launch_all: k_tpl_lane alone)
   bool ran_optimistic;     // (out) this decode was launched optimistically: it is complete only once
-                           // the host has read kInfoNeedFull as 0 (else it is re-run in full)
+                           // the host has read kInfoResid as 0 (else it is re-run in full)
+  bool ord_const;          // every learned shape has every slot at the same key position
+  uint32_t implicit;       // (out) TFRG_IMPLICIT_* columns the decode did not store
 };
 
 // Kernel stages, in launch order (profiling events bracket each one).

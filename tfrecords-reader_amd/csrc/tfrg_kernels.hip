@@ -3455,6 +3455,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // re-run by the host (tfrg_result_info) if a record took no template. Saves five dependent
   // launches (~4 us each) per batch.
   cfg.ran_optimistic = cfg.optimistic && quiet && all_spec && S > 0;
+  cfg.implicit = 0;
   DevOut ox = o;
   if (!lean) {
     ox.lmask = nullptr;
@@ -3468,6 +3469,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     a.lane_max = cfg.lane_max;
     a.tsum = cfg.ran_optimistic ? nullptr : o.tsum;  // (placed slots: no scan; a re-run clears tsum)
     a.finish = cfg.ran_optimistic ? sc.slot_kind : nullptr;
+    // (optimistic: status / verdict and constant order words are implicit, tfrg_info.implicit_cols)
+    cfg.implicit = cfg.ran_optimistic ? TFRG_IMPLICIT_STATUS | (cfg.ord_const ? TFRG_IMPLICIT_ORDER : 0u) : 0u;
+    a.implicit = cfg.implicit;
     a.n_slots = (uint32_t)S;
     a.tile_stride = o.tile_stride;
     const uint64_t n = b.n;

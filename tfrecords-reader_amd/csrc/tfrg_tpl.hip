@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       cand = act && !ok ? meta.z : 0xffu;
     }
     const bool hit = tsel != 0xffu;
-    if (hit) {
+    if (hit && !(A.implicit & TFRG_IMPLICIT_STATUS)) {  // (uniform test)
       o.status[r] = TFRG_OK;
       o.verdict[r] = (uint8_t)kHitVerdict;
     }
@@ -313,7 +313,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
                                                : wave_sum(hit ? (cw & ~kCountInline) : 0u);
         const LeanTgt& T = A.tg[k];
         if (hit) {
-          T.ord[r] = (uint16_t)(z.x >> 16);
+          if (!(A.implicit & TFRG_IMPLICIT_ORDER)) T.ord[r] = (uint16_t)(z.x >> 16);
           if (T.kind) {  // speculative placement: value at column row r; the row split r is implicit
                          // (tfrg_info.placed_slots: a final placement's row splits are never stored)
             if (r < T.lim) {

@@ -40,7 +40,7 @@ class TfrgInfo(C.Structure):
         ("nbytes", C.c_uint64),
         ("bytes_data_len", C.c_uint64),
         ("tpl_groups_missed", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("implicit_cols", C.c_uint32),
         ("placed_slots", C.c_uint64),
     ]
 
