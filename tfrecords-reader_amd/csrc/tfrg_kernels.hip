@@ -2334,12 +2334,12 @@ struct Pref {  // named fields, returned by value: an array or an out-parameter 
 };
 
 #define TFRG_PREF_LOAD(j)                                                        \
-  {                                                                              \
+  if constexpr ((j) < kPrefWords) {                                              \
     const uint64_t q = lo16 + lane * 16u + (uint32_t)(j)*1024u;                  \
     p.w##j = *reinterpret_cast<const uint4*>(src + (q < hi ? q : lo16c));         \
   }
 #define TFRG_PREF_STORE(j)                                                       \
-  {                                                                              \
+  if constexpr ((j) < kPrefWords) {                                              \
     const uint32_t off = lane * 16u + (uint32_t)(j) * 1024u;                     \
     if (lo16 + off < hi) *reinterpret_cast<uint4*>(dst + off) = p.w##j;          \
   }
