@@ -582,9 +582,9 @@ def run(args) -> None:
                 cw = c4_workload("c1v", 0, 8, args.files, "c4_c1v_rank0of8")
             else:
                 cw = single_workload(name)
-            # (a small batch's step is tens of microseconds: enough steps for a timed region of a few
-            # milliseconds, so the first launch after the idle synchronize does not weigh as a step)
-            c_steps = max(5, args.steps // 2, min(500, int(1e11 // max(cw.framed_bytes, 1))))
+            # (steps for a timed region of ~100 ms, as the headline's: the first launch after the idle
+            # synchronize costs ~0.3 ms once, and a small batch's step is tens of microseconds)
+            c_steps = max(5, args.steps // 2, min(500, int(4e11 // max(cw.framed_bytes, 1))))
             m = measure(ctx, cw, c_steps, max(args.warmup, min(50, c_steps // 10)), args.profile_steps)
             m["steps"] = c_steps
             del m["_d_bytes"], m["_elapsed"]

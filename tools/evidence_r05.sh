@@ -7,7 +7,7 @@
 #           statistics of the headline line and kernel traces of the small configs; part 3: the end-to-end runs and the GPU suite.
 #   bash tools/evidence_r05.sh 1|2|3
 set -u
-O=gpurun_out/r5e; mkdir -p $O/traffic
+O=gpurun_out/r5f2; mkdir -p $O/traffic
 export TMPDIR=/tmp
 if [ "$1" = 1 ]; then
   for spec in "c4 k_tpl_lane" "c4of8 k_tpl_lane" "c4of8v k_tpl_lane" "c1file k_tpl_lane" "c2 k_tail_count" "c3 k_tail_gather" "c4c2 k_tail_count"; do
@@ -21,6 +21,9 @@ elif [ "$1" = 2 ]; then
   tail -c 400 $O/bench.json
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rp -o run -- python bench.py --only c4 --no-cpu --steps 5 > $O/rp.log 2>&1 || { tail $O/rp.log; exit 1; }
   cp "$(find $O/rp -name '*kernel_stats.csv' -print -quit)" $O/rocprof_kernel_stats_r05.csv
+  # the same batches on one stream: no two lane kernels overlap, so each launch's duration is its own
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rp1 -o run -- python bench.py --only c4 --no-cpu --steps 5 --streams 1 > $O/rp1.log 2>&1 || { tail $O/rp1.log; exit 1; }
+  cp "$(find $O/rp1 -name '*kernel_stats.csv' -print -quit)" $O/rocprof_kernel_stats_c4_1stream_r05.csv
   for c in c1file c2 c4of8; do
     timeout -k 10 400 python tools/kernel_trace.py $O/kt_$c $c 30 > $O/kt_$c.log 2>&1 || { tail -20 $O/kt_$c.log; exit 1; }
   done
