@@ -69,7 +69,7 @@ VARIANTS = {
              "__launch_bounds__(kTplBlock, W == 16 ? 8 : (W == 32 ? 4 : 2))")],
     # k_tail_gather without the float copies / the packed int64 decode / int64_ring's pass B
     # (VALU attribution by PMC; wrong results)
-    "g_nofloat": [("tfrg_kernels.hip", "  uint64_t m = __ballot(packed && kind == TFRG_KIND_FLOAT);", "  uint64_t m = 0;")],
+    "g_nofloat": [("tfrg_kernels.hip", "  uint64_t m = __ballot(isf);", "  uint64_t m = 0;")],
     "g_noint64": [("tfrg_kernels.hip", "  int rr = int64_ring<COMPAT>(fs, o, iv, bo, bl, cnt, dst, lane, ring);", "  int rr = 1;")],
     "g_nopassb": [("tfrg_kernels.hip", "    while (gtot - gb >= 64u) pass_b(64u);\n", "    gb = gtot;\n"),
                   ("tfrg_kernels.hip", "  if (gtot > gb) pass_b(gtot - gb);", "  gb = gtot;")],
