@@ -94,17 +94,6 @@ VARIANTS = {
                   "  const uint64_t pmask = sc.spec ? (uint64_t)__ballot(lane < S && spec_placed(sc.spec, o, lane)) : 0ull;\n",
                   "  uint64_t pmask = 0;\n  if (sc.spec)\n    for (uint32_t k = 0; k < S && k < 64u; ++k) pmask |= (uint64_t)spec_placed(sc.spec, o, k) << k;\n"
                   "  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)pmask);\n")],
-    # the lane kernel without its walks of records from HBM (they go to the exact walker; timing of
-    # k_lane_count only)
-    "nobigwalk": [("tfrg_kernels.hip", "    const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));",
-                   "    const bool bigw = false && fast_ok && valid && (!mine || (span_rec && !staged));")],
-    # the same walks without the frame verdicts of their records
-    "nobigfv": [("tfrg_kernels.hip", "        frame_verdicts<R, false>(B, v, T, nullptr, 0, crc_here);\n        sink.fast_reset(S);\n        if (strict_pass(B, v.verdict, crc_here)) {",
-                 "        sink.fast_reset(S);\n        if (strict_pass(B, v.verdict, crc_here)) {")],
-    "win0lb4": [("tfrg_kernels.hip", "const FastSrcG<MODE != 0> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};",
-                 "const FastSrcG<true> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};"),
-                ("tfrg_kernels.hip", "__global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_count",
-                 "__global__ __launch_bounds__(kLaneCountBlock, 4) void k_lane_count")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
 }
