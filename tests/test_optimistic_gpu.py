@@ -136,3 +136,31 @@ def test_device_view_confirms_an_optimistic_decode(monkeypatch):
     finally:
         on.close()
         full.close()
+
+
+def test_optimistic_with_materialized_bytes_and_strict_crc(monkeypatch):
+    """An optimistic decode with TFRG_FLAG_MATERIALIZE_BYTES gathers the same byte column; with
+    TFRG_FLAG_STRICT_CRC a record whose payload CRC fails takes no template, so the decode is re-run
+    in full and reports the reference error for it."""
+    on, full = _pair(monkeypatch)
+    try:
+        buf, st, en = synth.framed(synth.c1_payloads(3000))
+        on.decode(buf, st, en)
+        full.decode(buf, st, en)
+        buf, st, en = synth.framed(synth.c1_payloads(5000, offset=11))
+        a = on.decode(buf, st, en, materialize_bytes=True)
+        b = full.decode(buf, st, en, materialize_bytes=True)
+        assert int(a.info.implicit_cols) == 3 and on.device_bytes()[1] == 0
+        _same(a, b)
+        assert np.array_equal(np.array(a.bytes_offsets), np.array(b.bytes_offsets))
+        assert bytes(np.array(a.bytes_data)) == bytes(np.array(b.bytes_data))
+        bad = buf.copy()
+        bad[int(st[1234]) + 12 + 3] ^= 0x20  # a payload byte of record 1234: its data CRC fails
+        a = on.decode(bad, st, en, strict_crc=True)
+        b = full.decode(bad, st, en, strict_crc=True)
+        assert on.device_bytes()[1] == 1  # (re-run in full)
+        _same(a, b)
+        assert int(a.status[1234]) != 0 and int(a.info.n_errors) == 1
+    finally:
+        on.close()
+        full.close()
