@@ -28,10 +28,10 @@ def _c1_odd(n: int, every: int) -> list[bytes]:
 
 
 def _pair(monkeypatch):
+    monkeypatch.setenv("TFRG_OPTIMISTIC", "1")  # (read at context creation; the suite may run with 0)
     on = hip.HipDecoder(0)
-    monkeypatch.setenv("TFRG_OPTIMISTIC", "0")  # (read at context creation)
+    monkeypatch.setenv("TFRG_OPTIMISTIC", "0")
     full = hip.HipDecoder(0)
-    monkeypatch.delenv("TFRG_OPTIMISTIC")
     return on, full
 
 
