@@ -105,7 +105,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // passes after k_tpl_lane would have nothing to do but their bookkeeping, done here: the next
 // decode's info words zeroed (k_lane_count), slot totals n, column bases and kind totals (k_spine's
 // every-slot-placed path), the last row split of every slot and the placed mask (k_down_gather). A
-// group listed (a record no template took, or one that failed): kInfoNeedFull, and the host re-runs
+// group listed (a record no template took, or one that failed): kInfoResid is not 0, and the host re-runs
 // the decode with every pass (tfrg_result_info). Saves the five dependent launches after it.
 // `listed`: the groups every workgroup listed, from the same atomic as the workgroup tickets (no
 // fence: a release per workgroup would write back the XCD's L2 every time).
