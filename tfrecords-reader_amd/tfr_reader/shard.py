@@ -105,9 +105,10 @@ DEFAULT_BATCH_BYTES = 1 << 30
 
 
 def plan_batches(starts: np.ndarray, ends: np.ndarray, batch_bytes: int = DEFAULT_BATCH_BYTES,
-                 nbytes: int | None = None) -> np.ndarray:
+                 nbytes: int | None = None, balanced: bool = True) -> np.ndarray:
     """Cut records (non-decreasing starts: one shard image in file order) into contiguous runs
-    whose byte span is at most ``batch_bytes``. Returns rows (r0, r1, lo, hi): records [r0, r1)
+    whose byte span is at most ``batch_bytes`` (``balanced``: the fewest such runs, of nearly equal
+    spans). Returns rows (r0, r1, lo, hi): records [r0, r1)
     read bytes [lo, hi), lo aligned down to 16 so a batch's base keeps the 16-byte alignment of the
     image. ``nbytes`` (the image size) clamps a last record that runs past EOF (indexer.pyx:225-249
     indexes it; it decodes as truncated)."""
@@ -121,11 +122,16 @@ def plan_batches(starts: np.ndarray, ends: np.ndarray, batch_bytes: int = DEFAUL
     top = np.maximum.accumulate(np.maximum(en, st)) if n else en
     if nbytes is not None:
         top = np.minimum(top, np.uint64(nbytes))
+    # as few batches as the cap allows, of nearly equal spans (a last batch much smaller than the
+    # others would run alone at the end of a step on two streams)
+    span = int(top[-1]) - (int(st[0]) & ~15) if n else 0
+    k = max(1, -(-span // batch_bytes))
+    target = min(batch_bytes, -(-span // k) + 4096) if balanced else batch_bytes
     rows = []
     r0 = 0
     while r0 < n:
         lo = int(st[r0]) & ~15
-        r1 = int(np.searchsorted(top, np.uint64(lo + batch_bytes), side="right"))
+        r1 = int(np.searchsorted(top, np.uint64(lo + target), side="right"))
         if r1 <= r0:
             r1 = r0 + 1  # one record wider than a batch: alone (the device rejects it if >= 4 GiB)
         r1 = min(r1, r0 + (1 << 30))
