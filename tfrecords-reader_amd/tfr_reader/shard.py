@@ -126,6 +126,7 @@ def plan_batches(starts: np.ndarray, ends: np.ndarray, batch_bytes: int = DEFAUL
     # others would run alone at the end of a step on two streams)
     span = int(top[-1]) - (int(st[0]) & ~15) if n else 0
     k = max(1, -(-span // batch_bytes))
+    balanced = balanced and os.environ.get("TFRG_PLAN_BALANCED", "1") != "0"  # (A/B measurements)
     target = min(batch_bytes, -(-span // k) + 4096) if balanced else batch_bytes
     rows = []
     r0 = 0
