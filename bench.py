@@ -276,6 +276,11 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         infos = sd.infos(plan)
     _check(infos)
 
+    # a one-line marker kernel (k_stream_read over 16 bytes) on the main stream, before the timed
+    # steps: profilers tell this workload's full-batch dispatches (every one after it) from the
+    # learning sample's decodes before it (tools/_dispatch.py)
+    _mark(ctx, d_bytes)
+
     # ---- timed region: barrier + synchronize on both sides, max over ranks
     if ctx.dist:
         import torch.distributed as tdist
@@ -453,6 +458,15 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         out["roofline"]["traffic"], out["roofline"]["traffic_source"] = traffic
     sd.close()
     return out
+
+
+def _mark(ctx: Ctx, d_bytes) -> None:
+    from tfr_reader import _native
+
+    sink = torch.zeros(4, dtype=torch.int32, device=ctx.dev)
+    _native.check(_native.lib().tfrg_stream_read(d_bytes.data_ptr(), 16, sink.data_ptr(), ctx.stream.cuda_stream, 0),
+                  "tfrg_stream_read")
+    torch.cuda.synchronize(ctx.dev)
 
 
 def _present_lists(dec, w: Workload) -> float:

@@ -126,15 +126,24 @@ int tfrg_ctx_device_bytes(tfrg_ctx* ctx, uint64_t* bytes, uint64_t* hint_reruns)
  * 0 routes every wavefront record to the streaming kernels). A tuning/testing knob. */
 int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
 
-/* Record-shape templates (no reference counterpart: a fast path under decoder.pyx:107-300). Up to 4
- * shapes of canonical records (payload <= 240 bytes) -- every byte fixed except list contents, incl.
- * the continuation bits of packed int64 lists -- are learned from up to 4,096 host records; a framed
- * record equal to a template under its mask, with matching length field and CRCs, gets the
- * template's dict without a walk (its values are still read from the record; k_tpl_lane, schemas of
- * <= 16 slots, CRC verdicts on). Learned automatically from the first tfrg_decode_host
- * batch after each tfrg_set_schema; device-only callers pass a host sample here. Returns the number
- * of templates (0..4). tfrg_ctx_set_templates(ctx, 0) disables the match (env TFRG_TEMPLATES=0);
- * the speculative placement of slots that are one inline value in every learned shape stays on. */
+/* Record-shape templates (no reference counterpart: a fast path under decoder.pyx:107-300). Up to
+ * TFRG_TPL_MAX shapes of canonical records (payload <= TFRG_TPL_MAX_PAYLOAD bytes, at most
+ * TFRG_TPL_MAX_ENTRIES feature entries) -- every byte fixed except list contents, incl. the
+ * continuation bits of packed int64 lists -- are learned from up to TFRG_TPL_SAMPLE host records
+ * spread over the batch, the most frequent shapes first (a shape seen once in a sample of >= 256 is
+ * not kept; with payloads over 112 bytes the lane image holds at most 30, the LDS beside the CRC
+ * tables). A framed record equal to a template under its mask, with matching length field and CRCs,
+ * gets the template's dict without a walk (its values are still read from the record; k_tpl_lane,
+ * schemas of <= TFRG_TPL_MAX_SLOTS slots, CRC verdicts on); any other record takes the canonical walk.
+ * Learned automatically from the first tfrg_decode_host batch after each tfrg_set_schema; device-only
+ * callers pass a host sample here. Returns the number of templates (0..TFRG_TPL_MAX).
+ * tfrg_ctx_set_templates(ctx, 0) disables the match (env TFRG_TEMPLATES=0); the speculative
+ * placement of slots that are one inline value in every learned shape stays on. */
+#define TFRG_TPL_MAX 32
+#define TFRG_TPL_MAX_PAYLOAD 240
+#define TFRG_TPL_MAX_ENTRIES 16
+#define TFRG_TPL_MAX_SLOTS 16
+#define TFRG_TPL_SAMPLE 4096
 int tfrg_learn_templates(tfrg_ctx* ctx, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                          const uint64_t* h_end, uint32_t n, uint32_t flags);
 int tfrg_template_count(tfrg_ctx* ctx);

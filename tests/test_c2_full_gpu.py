@@ -23,11 +23,12 @@ from tfr_reader import shard, synth
 pytestmark = pytest.mark.gpu
 
 
-def _decode_like_bench(buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, batch_bytes: int):
+def _decode_like_bench(buf: np.ndarray, starts: np.ndarray, ends: np.ndarray, batch_bytes: int,
+                       balanced: bool = True):
     import torch
 
     dev = torch.device("cuda", 0)
-    sd = shard.ShardDecoder(0, batch_bytes, 2)
+    sd = shard.ShardDecoder(0, batch_bytes, 2, balanced=balanced)
     try:
         plan = sd.plan(starts, ends, int(buf.size))
         rst, ren = sd.rebase(plan, starts, ends)
@@ -76,7 +77,8 @@ def test_c2_directory_2gib_batch_values():
         f += 1
     sb = shard.ShardBatch([synth.c4_file_name(i) for i in range(f)], imgs)
     del imgs
-    plan, res = _decode_like_bench(sb.buf, sb.starts, sb.ends, 1 << 31)
+    # balanced=False: one batch as wide as the cap (u32 offsets up to 2^31), not k equal ones
+    plan, res = _decode_like_bench(sb.buf, sb.starts, sb.ends, 1 << 31, balanced=False)
     assert len(plan) >= 2 and int((plan[:, 3] - plan[:, 2]).max()) > (1 << 31) - (1 << 20)
     n = len(sb)
     assert len(res) == n and (res.status == 0).all() and (res.verdict == 7).all()

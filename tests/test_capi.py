@@ -52,3 +52,25 @@ def test_status_messages_match_the_python_mirror():
     assert lib.tfrg_status_message(S.ERR_WIRE_TYPE, 4).decode() == "Unsupported wire type: 4"
     assert lib.tfrg_status_exception(S.ERR_KEY_UTF8).decode() == "UnicodeDecodeError"
     assert lib.tfrg_status_exception(0).decode() == ""
+
+
+def test_header_template_limits_match_the_kernel_constants():
+    """include/tfrg.h's numeric template limits are the ones csrc/tfrg_internal.h builds with."""
+    root = Path(__file__).resolve().parents[1]
+    hdr = (root / "include" / "tfrg.h").read_text()
+    internal = (root / "tfrecords-reader_amd" / "csrc" / "tfrg_internal.h").read_text()
+    capi = (root / "tfrecords-reader_amd" / "csrc" / "tfrg_capi.cpp").read_text()
+
+    def macro(name):
+        return int(re.search(rf"#define {name} (\d+)", hdr).group(1))
+
+    def const(name):
+        return int(re.search(rf"\b{name} = (\d+)", internal).group(1))
+
+    assert macro("TFRG_TPL_MAX") == const("kTplMaxLane")
+    assert macro("TFRG_TPL_MAX_PAYLOAD") == const("kTplMaxL")
+    assert macro("TFRG_TPL_MAX_ENTRIES") == const("kTplMaxEntries")
+    assert macro("TFRG_TPL_MAX_SLOTS") == const("kLeanMaxSlots")
+    lim = re.search(r"const uint32_t lim = n < (\d+)u \? n : (\d+)u;", capi)
+    assert lim and int(lim.group(1)) == int(lim.group(2)) == macro("TFRG_TPL_SAMPLE")
+    assert "Up to 4" not in hdr and "(0..4)" not in hdr

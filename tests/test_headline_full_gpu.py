@@ -46,7 +46,9 @@ def _check(mine: list[int], batch_bytes: int | None) -> None:
     del imgs
     n = len(sb)
     dev = torch.device("cuda", 0)
-    sd = shard.ShardDecoder(0, batch_bytes) if batch_bytes else shard.ShardDecoder(0)
+    # a given batch size: the greedy plan (balanced=False), so one batch is as wide as the cap and the
+    # u32 offsets reach 2^31 - 2; the default: the library's balanced plan
+    sd = shard.ShardDecoder(0, batch_bytes, balanced=False) if batch_bytes else shard.ShardDecoder(0)
     try:
         plan = sd.plan(sb.starts, sb.ends, sb.nbytes)
         if batch_bytes:

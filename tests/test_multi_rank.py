@@ -115,6 +115,38 @@ def test_plan_batches_properties():
         shard.plan_batches(st[::-1].copy(), en[::-1].copy(), 4096)
 
 
+@pytest.mark.parametrize("shape", ["c1", "c2", "mixed"])
+def test_plan_batches_balanced_exactly_k(shape):
+    """The balanced plan: exactly k = ceil(span / cap) batches, each within one record (the largest)
+    of span / k — no (k+1)-th sliver batch however large the records are against the cap's slack —
+    and the greedy plan (balanced=False) keeps a batch as wide as the cap allows."""
+    from tfr_reader import shard
+
+    rng = np.random.default_rng({"c1": 1, "c2": 2, "mixed": 3}[shape])
+    if shape == "c1":
+        lens = rng.choice(np.array([58, 59], np.uint64), 400_000)
+    elif shape == "c2":  # oxford_flowers102-shaped: lognormal around 40 KiB, up to 512 KiB
+        lens = np.clip(rng.lognormal(np.log(40 << 10), 0.6, 20_000), 1 << 10, 512 << 10).astype(np.uint64)
+    else:
+        lens = np.where(rng.random(50_000) < 0.02, rng.integers(1 << 16, 1 << 19, 50_000),
+                        rng.integers(20, 300, 50_000)).astype(np.uint64)
+    en = np.cumsum(lens, dtype=np.uint64)
+    st = en - lens
+    span = int(en[-1])
+    big = int(lens.max())
+    for k_want in (1, 2, 3, 4, 7):
+        cap = -(-span // k_want) + (span // 1000 if k_want > 1 else 0)  # ceil(span / cap) == k_want
+        k = -(-span // cap)
+        plan = shard.plan_batches(st, en, cap, span)
+        assert len(plan) == k, (k, plan)
+        assert plan[0, 0] == 0 and plan[-1, 1] == st.size and (plan[1:, 0] == plan[:-1, 1]).all()
+        widths = plan[:, 3] - plan[:, 2]
+        assert (widths <= cap).all()
+        assert (np.abs(widths - span / k) <= big + 16).all(), (widths, span / k, big)
+        greedy = shard.plan_batches(st, en, cap, span, balanced=False)
+        assert int((greedy[:, 3] - greedy[:, 2]).max()) > cap - big - 16
+
+
 def test_rebase32_back_to_back_and_gaps():
     """u32 per-batch offsets (tfrg_decode_device32): ends alone for back-to-back records, explicit
     starts as soon as one record does not start where the previous one ended."""

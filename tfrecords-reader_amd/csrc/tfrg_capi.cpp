@@ -157,6 +157,7 @@ struct tfrg_ctx {
   bool ord_const = false;     // (Learned::ord_const) of the learned shapes
   uint32_t last_implicit = 0; // TFRG_IMPLICIT_* columns the last decode did not store
   bool cols_complete = false; // tfrg_result_device filled them into the device columns
+  bool mat_pending = false;   // an optimistic decode's byte materialization waits for its confirmation
   struct LastCall {
     const uint8_t* d_bytes;
     uint64_t nbytes;
@@ -601,8 +602,16 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
   for (auto& kv : seen)
     if (kv.second.first >= min_count) order.push_back({kv.second.first, &kv.second.second});
   std::stable_sort(order.begin(), order.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-  const uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMaxLane);
+  uint32_t nt = (uint32_t)std::min<size_t>(order.size(), kTplMaxLane);
   if (!nt) return 0;
+  // the window the longest kept shape needs, and as many templates as fit LDS beside the CRC tables
+  // at that window (the least frequent dropped first; a smaller maximum length may shrink W again)
+  auto window_of = [&](uint32_t m) {
+    uint32_t mx = 0;
+    for (uint32_t k = 0; k < m; ++k) mx = std::max(mx, order[k].second->L);
+    return mx + 16 <= 64 ? 16u : (mx + 16 <= 128 ? 32u : 64u);
+  };
+  while (nt > 1 && kLiTpl + (uint64_t)nt * kLiTw(window_of(nt)) > kLiMaxWords) --nt;
   uint64_t kept = 0;
   for (uint32_t k = 0; k < nt; ++k) kept += order[k].first;
   out.full = kept == lim;
@@ -631,9 +640,7 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
     }
   }
   // window form (tfrg_internal.h): the last 4 W bytes of every kept shape's framed record
-  uint32_t maxL = 0;
-  for (uint32_t k = 0; k < nt; ++k) maxL = std::max(maxL, order[k].second->L);
-  const uint32_t W = maxL + 16 <= 64 ? 16u : (maxL + 16 <= 128 ? 32u : 64u);
+  const uint32_t W = window_of(nt);
   const CrcTables& CT = crc_tables();
   std::vector<uint32_t> w((size_t)nt * kLtWords, 0);
   for (uint32_t k = 0; k < nt; ++k) {
@@ -864,6 +871,30 @@ int tfrg_decode_device32(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, c
   return decode_device_any(c, d_bytes, nbytes, off, n, flags, stream);
 }
 
+// TFRG_FLAG_MATERIALIZE_BYTES: the bytes views of the decode just enqueued on `st` gathered into one
+// contiguous column. Reads the decode's kind totals and b_off / b_len, so it runs only once they are
+// final: after a full decode at once, after an optimistic one once finish_decode has confirmed it.
+static hipError_t launch_materialize_last(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, uint64_t cap_in,
+                                          uint64_t cap_b, hipStream_t st) {
+  uint32_t* const info = c->info.as<uint32_t>() + c->info_slot * kInfoCount;
+  DevBytes d;
+  d.in = d_bytes;
+  d.in_readable = (nbytes + 15) & ~15ull;
+  d.b_off = c->b_off.as<uint32_t>();
+  d.b_len = c->b_len.as<uint32_t>();
+  d.kind_totals = c->kind_totals.as<uint64_t>();
+  d.offsets = c->boff64.as<uint64_t>();
+  d.offsets_cap = cap_b;
+  d.data = c->bdata.as<uint8_t>();
+  d.data_cap = cap_in + 16;
+  d.lb = c->blb.as<uint64_t>();
+  d.ticket = info + kInfoBytesTicket;
+  d.big_count = info + kInfoBytesBig;
+  d.big_list = c->bbig.as<uint32_t>();
+  d.overflow = info + kInfoOverflow;
+  return launch_materialize(d, c->num_cus, st);
+}
+
 static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbytes, const Offsets& off, uint32_t n,
                              uint32_t flags, void* stream) {
   if (!c) return TFRG_E_ARG;
@@ -1066,24 +1097,11 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
       ev = c->ev;
     }
     hipError_t e = launch_decode(b, schema_view(c), o, cfg, c->crc_tab.as<uint32_t>(), c->consts.as<uint32_t>(), st, ev);
-    if (e == hipSuccess && mat && S) {
-      DevBytes d;
-      d.in = d_bytes;
-      d.in_readable = (nbytes + 15) & ~15ull;
-      d.b_off = o.b_off;
-      d.b_len = o.b_len;
-      d.kind_totals = o.kind_totals;
-      d.offsets = c->boff64.as<uint64_t>();
-      d.offsets_cap = cap_b;
-      d.data = c->bdata.as<uint8_t>();
-      d.data_cap = cap_in + 16;
-      d.lb = c->blb.as<uint64_t>();
-      d.ticket = o.info + kInfoBytesTicket;
-      d.big_count = o.info + kInfoBytesBig;
-      d.big_list = c->bbig.as<uint32_t>();
-      d.overflow = o.info + kInfoOverflow;
-      e = launch_materialize(d, c->num_cus, st);
-    } else if (e == hipSuccess && mat) {
+    // (an optimistic decode that leaves records writes no kind totals and is re-run in full: its
+    // byte views are gathered only once finish_decode has confirmed it)
+    if (e == hipSuccess && mat && S && !cfg.ran_optimistic) {
+      e = launch_materialize_last(c, d_bytes, nbytes, cap_in, cap_b, st);
+    } else if (e == hipSuccess && mat && !S) {
       e = hipMemsetAsync(c->boff64.p, 0, 8, st);  // no slots: no elements
     }
     if (ev && e == hipSuccess) e = hipEventRecord(ev[kNumStages], st);
@@ -1104,6 +1122,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   c->have_result = true;
   c->rs_complete = false;
   c->opt_pending = n != 0 && cfg.ran_optimistic;
+  c->mat_pending = c->opt_pending && mat && S;
   c->last_implicit = n != 0 ? cfg.implicit : 0u;
   c->cols_complete = false;
   return 0;
@@ -1156,7 +1175,15 @@ static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
     HIP_TRY(hipStreamSynchronize(c->last_stream));
     const bool full = c->opt_pending && h[kInfoResid] != 0;  // (records no template took)
     const bool widen = h[kInfoOverflow] && c->hinted && !widened;
-    if (!full && !widen) break;
+    if (!full && !widen) {
+      if (!c->mat_pending) break;
+      // a confirmed optimistic decode: its byte views now, then its info words again (the gather
+      // reports an overflow there)
+      c->mat_pending = false;
+      const tfrg_ctx::LastCall& L = c->last;
+      HIP_TRY(launch_materialize_last(c, L.d_bytes, L.nbytes, L.cap_in, c->cap_b, c->last_stream));
+      continue;
+    }
     const tfrg_ctx::LastCall L = c->last;
     c->no_quiet = true;
     c->no_hints = widen;
@@ -1171,6 +1198,7 @@ static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
     ++c->hint_reruns;
   }
   c->opt_pending = false;
+  c->hinted = false;  // (confirmed: the capacities held, or the worst-case re-run replaced it)
   return 0;
 }
 
@@ -1211,12 +1239,19 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
 
 int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
   if (!c || !c->have_result) return TFRG_E_ARG;
-  if (c->opt_pending) {  // an optimistic decode: confirmed (or re-run in full) before the view
+  // an optimistic decode, or one whose value capacities were hinted below the worst case: confirmed
+  // (or re-run in full / at the worst case) before the view, as tfrg_result_info does
+  if (c->opt_pending || c->hinted) {
     HIP_TRY(hipSetDevice(c->device));
     uint32_t h[kInfoCount];
     uint64_t kt[4];
     const int rc = finish_decode(c, h, kt);
     if (rc) return rc;
+    if (h[kInfoOverflow]) {
+      set_error("value columns overflowed their capacity (overlapping ranges in a device batch): decode "
+                "the ranges from host memory (tfrg_decode_host) or split the batch");
+      return TFRG_E_LIMIT;
+    }
   }
   if (!c->rs_complete && c->n_slots && c->n) {
     // a self-consistent view: the identity rows of the finally placed slots, which the decode does

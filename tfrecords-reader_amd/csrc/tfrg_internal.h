@@ -55,7 +55,7 @@ struct DevSchema {
 // [kLtSlot + 3 k] the same entries by SLOT k (< kLeanMaxSlots), so that k_tpl_lane stores slot k's
 // columns once for the lanes of every template: {mode | len << 8 | rank << 16 (0: absent), pos,
 // count word (0: absent)}.
-constexpr uint32_t kTplMaxL = 240, kTplMaxEntries = 16, kTplMax = 4;
+constexpr uint32_t kTplMaxL = 240, kTplMaxEntries = 16;  // (tfrg.h TFRG_TPL_MAX_PAYLOAD / _ENTRIES)
 constexpr uint32_t kLtMaxW = 64;
 constexpr uint32_t kLeanMaxSlots = 16;  // k_tpl_lane runs for schemas of at most this many slots
 constexpr uint32_t kLtL = 0, kLtNe = 1, kLtCrcw = 2, kLtChain = 3, kLtK = 4, kLtAbsent = 5, kLtEnt = 8,
@@ -78,11 +78,15 @@ constexpr uint32_t kLeanTabOff = 51200;  // crc_tab words: T_d, d < 32, 256 entr
 //     (0xff: none), [4, 4 + W) Bm, [4 + W, 4 + 2 W) Mm, [4 + 2 W, 4 + 3 W) Cm, then per slot k 4 words
 //     {mode | len << 8 | rank << 16 (0: absent), pos, count word (0: absent), 0}
 //     (tfrg_internal.h "Record-shape template" for the fields).
-constexpr uint32_t kTplMaxLane = 32;  // templates kept for the lane kernel (the most frequent shapes)
+constexpr uint32_t kTplMaxLane = 32;  // templates kept for the lane kernel (the most frequent shapes; TFRG_TPL_MAX)
 constexpr uint32_t kLiHdr = 8, kLiSlotQ = kLiHdr, kLiLut = kLiSlotQ + kLeanMaxSlots,
                    kLiLutWords = (kTplMaxL + 1 + 3) / 4, kLiTpl = (kLiLut + kLiLutWords + 3) & ~3u;
 constexpr uint32_t kLiQValue = 1u << 16, kLiQSingle = 1u << 17;
 __host__ __device__ constexpr uint32_t kLiTw(uint32_t W) { return 4 + 3 * W + 4 * kLeanMaxSlots; }
+// LDS words the lane image may take: a workgroup's 64 KiB less k_tpl_lane's static 32 KiB of CRC
+// tables and 512 B for its other static words (tfrg_tpl.hip asserts it). With W = 64 this keeps 30
+// templates, not kTplMaxLane (learn_shapes drops the least frequent ones).
+constexpr uint32_t kLiMaxWords = (65536u - 32768u - 512u) / 4u;
 
 // Column targets of one slot for k_tpl_lane, computed on the host per decode.
 struct LeanTgt {

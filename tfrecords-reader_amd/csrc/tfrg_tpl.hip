@@ -33,6 +33,7 @@ namespace {
 
 constexpr int kTplBlock = 512;        // 8 waves: the 32 KiB of tables are shared by 8 waves
 constexpr uint32_t kTplTabs = 32;     // T_0 .. T_31
+static_assert(4u * kTplTabs * 256u + 4u * kLiMaxWords + 512u <= 65536u, "lane image + CRC tables exceed LDS");
 constexpr uint32_t kHitVerdict = TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC;
 #ifndef TFRG_TPL_GROUPS_PER_STEP
 #define TFRG_TPL_GROUPS_PER_STEP 1

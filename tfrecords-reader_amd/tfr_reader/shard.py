@@ -122,17 +122,61 @@ def plan_batches(starts: np.ndarray, ends: np.ndarray, batch_bytes: int = DEFAUL
     top = np.maximum.accumulate(np.maximum(en, st)) if n else en
     if nbytes is not None:
         top = np.minimum(top, np.uint64(nbytes))
-    # as few batches as the cap allows, of nearly equal spans (a last batch much smaller than the
-    # others would run alone at the end of a step on two streams)
-    span = int(top[-1]) - (int(st[0]) & ~15) if n else 0
-    k = max(1, -(-span // batch_bytes))
+    if not n:
+        return np.zeros((0, 4), np.int64)
     balanced = balanced and os.environ.get("TFRG_PLAN_BALANCED", "1") != "0"  # (A/B measurements)
-    target = min(batch_bytes, -(-span // k) + 4096) if balanced else batch_bytes
+    if balanced:
+        rows = _balanced_rows(st, top, batch_bytes)
+        if rows is not None:
+            return rows
+    return _greedy_rows(st, top, batch_bytes)
+
+
+def _rows_from_cuts(st: np.ndarray, top: np.ndarray, cuts: np.ndarray) -> np.ndarray:
+    """Rows (r0, r1, lo, hi) of the record runs between consecutive cut indices (0 and n included)."""
+    r0, r1 = cuts[:-1], cuts[1:]
+    lo = (st[r0].astype(np.int64)) & ~15
+    hi = np.maximum(top[r1 - 1].astype(np.int64), lo)
+    return np.stack([r0, r1, lo, hi], axis=1).astype(np.int64)
+
+
+def _balanced_rows(st: np.ndarray, top: np.ndarray, cap: int) -> np.ndarray | None:
+    """The fewest batches the cap allows, k = ceil(span / cap), of nearly equal spans: batch i starts
+    at the record boundary nearest lo0 + i * span / k, so each batch is within one record of span / k
+    and there is never a (k+1)-th sliver. k + 1 (then k + 2 …) only when such a cut would leave a
+    batch over the cap (records larger than the slack); None when no balanced plan fits (records
+    wider than the cap: the greedy plan puts them alone)."""
+    n = int(st.shape[0])
+    lo0 = int(st[0]) & ~15
+    span = int(top[-1]) - lo0
+    k0 = max(1, -(-span // cap))
+    sti = st.astype(np.int64)
+    for k in range(k0, min(n, k0 + 8) + 1):
+        if k == 1:
+            cuts = np.array([0, n], np.int64)
+        else:
+            t = lo0 + (np.arange(1, k, dtype=np.int64) * span) // k
+            c = np.searchsorted(sti, t, side="left")  # first record starting at or after t
+            c = np.clip(c, 1, n - 1)
+            prev = np.clip(c - 1, 1, n - 1)
+            c = np.where(np.abs(sti[prev] - t) < np.abs(sti[c] - t), prev, c)  # the nearer boundary
+            cuts = np.concatenate([[0], c, [n]]).astype(np.int64)
+            if (np.diff(cuts) <= 0).any():
+                continue
+        rows = _rows_from_cuts(st, top, cuts)
+        if ((rows[:, 3] - rows[:, 2]) <= cap).all() and ((rows[:, 1] - rows[:, 0]) <= 1 << 30).all():
+            return rows
+    return None
+
+
+def _greedy_rows(st: np.ndarray, top: np.ndarray, cap: int) -> np.ndarray:
+    """Each batch as wide as the cap allows (the last one takes what is left)."""
+    n = int(st.shape[0])
     rows = []
     r0 = 0
     while r0 < n:
         lo = int(st[r0]) & ~15
-        r1 = int(np.searchsorted(top, np.uint64(lo + target), side="right"))
+        r1 = int(np.searchsorted(top, np.uint64(lo + cap), side="right"))
         if r1 <= r0:
             r1 = r0 + 1  # one record wider than a batch: alone (the device rejects it if >= 4 GiB)
         r1 = min(r1, r0 + (1 << 30))
@@ -189,12 +233,13 @@ class ShardDecoder:
     pool over files (indexer.py:121-134) and a thread pool over records (reader.py:212-247)."""
 
     def __init__(self, device: int = 0, batch_bytes: int = DEFAULT_BATCH_BYTES, n_streams: int = 2,
-                 spec_varint: bool = False, keys=None, value_caps: bool = True) -> None:
+                 spec_varint: bool = False, keys=None, value_caps: bool = True, balanced: bool = True) -> None:
         from tfr_reader import hip
 
         self.device = device
         self.value_caps = value_caps  # learn(): size the value columns from the sample
         self.batch_bytes = int(batch_bytes)
+        self.balanced = balanced  # plan_batches: k equal batches (False: each as wide as the cap)
         self.n_streams = max(1, int(n_streams))
         self.spec_varint = spec_varint
         self.keys = keys or hip.KeyTable()
@@ -213,7 +258,7 @@ class ShardDecoder:
         return self.decs[:k]
 
     def plan(self, starts, ends, nbytes: int | None = None) -> np.ndarray:
-        return plan_batches(starts, ends, self.batch_bytes, nbytes)
+        return plan_batches(starts, ends, self.batch_bytes, nbytes, self.balanced)
 
     # ------------------------------------------------------------------ host input
     def decode(self, buf: np.ndarray, starts, ends, **kw) -> ShardResult:
