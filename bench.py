@@ -317,6 +317,29 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     # the last one stands for all of them)
     assert reruns == 0, f"{reruns} decodes re-run after the timed region"
 
+    # ---- what a device-resident consumer pays on top of the step (not part of `value`): an
+    # optimistic decode is complete once confirmed (tfrg_result_info: one host-synchronizing read of
+    # its info words per batch), and the device view (tfrg_result_device) writes the columns the
+    # decode left implicit (status / verdict / order, placed row splits). Steps on the same streams,
+    # each followed by the confirmation of every batch, then by the device view of every batch.
+    def consumer(view: bool, k: int) -> float:
+        torch.cuda.synchronize(dev)
+        t = time.perf_counter()
+        for _ in range(k):
+            step()
+            for d in sd.decs[: len(plan)]:
+                d.info()
+                if view:
+                    d.device_columns()
+            if view:
+                torch.cuda.synchronize(dev)
+        torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t) / k * 1e3
+
+    k_cons = max(3, min(steps, 20))
+    consumer(True, 1)
+    conf_ms, view_ms = consumer(False, k_cons), consumer(True, k_cons)
+
     # ---- per-kernel durations: HIP events recorded by libtfrg on the launch stream, the batches
     # run back to back on one stream so that no launch overlaps another batch's. Each profiled step
     # follows an unprofiled one on the same stream: the GPU is busy when its first kernel starts (a
@@ -362,14 +385,16 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         placed &= int(i.placed_slots)
     n_placed = bin(placed & ((1 << min(n_slots, 64)) - 1)).count("1")
     # columns an optimistic decode left implicit in every batch (tfrg_info.implicit_cols: constant
-    # status / verdict, constant order words), never stored: not counted
-    implicit = 3
+    # status / verdict, constant order words, constant bytes element lengths), never stored: not counted
+    implicit = 7
     for i in infos:
         implicit &= int(i.implicit_cols)
     st_b = 0 if implicit & 1 else 5
     ord_b = 0 if implicit & 2 else 2 * n_slots
     # (off_bytes: the record offsets as handed over -- 4 B of u32 ends, 8 B of u32 pairs, 16 B of u64)
-    lane_alg = small_bytes + n_small * (off_bytes + st_b + ord_b + 4 * (n_slots - n_placed)) + 8 * present_small
+    n_bytes_slots = sum(1 for k in sd.keys.slot_kind[:n_slots] if int(k) == 1)
+    len_b = 4 * n_small * n_bytes_slots if implicit & 4 else 0  # (the implicit bytes_len words)
+    lane_alg = small_bytes + n_small * (off_bytes + st_b + ord_b + 4 * (n_slots - n_placed)) + 8 * present_small - len_b
     alg = {
         # template path: its records' framed bytes + offsets in; status, verdict, order per slot, a row
         # split (or count) per slot not placed, and a value / location word per present list out
@@ -390,7 +415,8 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
     n_keys = len(sd.keys.keys)
     R = framed + off_bytes * n
     # (SURVEY D2's W, less the row splits of placed slots and the implicit status, never stored)
-    W = (0 if implicit & 1 else 4 * n) + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + 12 * kt[1]
+    W = (0 if implicit & 1 else 4 * n) + 4 * n * (n_keys - n_placed) + 8 * kt[3] + 4 * kt[2] + \
+        (8 if implicit & 4 else 12) * kt[1]
     ms_step = elapsed / steps * 1e3
     out = {
         "workload": w.desc,
@@ -413,6 +439,12 @@ def measure(ctx: Ctx, w: Workload, steps: int, warmup: int, prof_steps: int, tem
         # (the step is the larger of the host's wall clock and the GPU events: a small batch's step
         # can be the host's enqueue rate)
         "step_parts_ms": {"host_wall": round(wall / steps * 1e3, 4), "gpu_events": round(ev_s / steps * 1e3, 4)},
+        # a consumer's cost per step beyond the timed step (wall clock, k_cons steps each): the
+        # confirmation of every batch (host sync included), then the device view on top of it
+        "consumer": {"step_plus_confirm_ms": round(conf_ms, 4), "confirm_ms": round(conf_ms - ms_step, 4),
+                     "step_plus_confirm_view_ms": round(view_ms, 4), "device_view_ms": round(view_ms - conf_ms, 4),
+                     "GiB_s_confirmed": round(framed / (conf_ms / 1e3) / 2**30, 3),
+                     "GiB_s_confirmed_view": round(framed / (view_ms / 1e3) / 2**30, 3), "steps": k_cons},
         "GiB_s": round(framed / (ms_step / 1e3) / 2**30, 3),
         "examples_per_s": round(n / (ms_step / 1e3), 1),
         "kernels_ms": {k: round(v, 4) for k, v in kern_ms.items()},
@@ -656,6 +688,10 @@ def run(args) -> None:
             "roofline": head["roofline"],
             "pipeline": head["pipeline"],
             "cpu_baseline": cpu,
+            # a device-resident consumer's extra cost per step (measure(): consumer), not in `value`
+            "confirm_ms": head["consumer"]["confirm_ms"],
+            "device_view_ms": head["consumer"]["device_view_ms"],
+            "consumer": head["consumer"],
         }
         if configs:
             line["configs"] = configs

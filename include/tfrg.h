@@ -237,7 +237,9 @@ typedef struct tfrg_info {
   /* TFRG_IMPLICIT_* bits: columns an optimistic decode (tfrg_result_info) did not store because every
    * record of the batch took a record shape: STATUS -- every status 0 (aux unused) and every verdict
    * TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC; ORDER -- every slot's order word is the
-   * same for every record (its key position in the shapes). tfrg_result_fetch fills them into the
+   * same for every record (its key position in the shapes); BYTES_LEN -- every bytes_list slot holds
+   * one element per record whose length is the same in every shape (the bytes_len column is that
+   * constant; not with TFRG_FLAG_MATERIALIZE_BYTES). tfrg_result_fetch fills them into the
    * caller's buffers on the host (no copy), tfrg_result_device into the device columns (once per
    * decode, on the decode's stream, before it returns the view). */
   uint32_t implicit_cols;

@@ -70,5 +70,6 @@ enum tfrg_verdict {
 /* tfrg_info.implicit_cols (tfrg.h): columns an optimistic decode did not store */
 #define TFRG_IMPLICIT_STATUS 1u /* status 0, aux 0, verdict LEN_MATCH | LEN_CRC | DATA_CRC for every record */
 #define TFRG_IMPLICIT_ORDER 2u  /* every slot's order word the same for every record */
+#define TFRG_IMPLICIT_BYTES_LEN 4u /* every bytes_list slot one element of one length for every record */
 
 #endif

@@ -49,7 +49,8 @@ def test_optimistic_decode_identical_and_rerun_on_a_miss(monkeypatch):
         a, b = on.decode(buf, st, en), full.decode(buf, st, en)  # (learns the shapes: the whole sample)
         _same(a, b)
         assert int(a.info.tpl_groups_missed) == 0 and on.device_bytes()[1] == 0  # optimistic, complete
-        assert int(a.info.implicit_cols) == 3 and int(b.info.implicit_cols) == 0  # status / order constant
+        # status / order constant, and the 12-byte ids' lengths (TFRG_IMPLICIT_BYTES_LEN)
+        assert int(a.info.implicit_cols) == 7 and int(b.info.implicit_cols) == 0
         pl = _c1_odd(5000, 499)
         buf, st, en = synth.framed(pl)
         a, b = on.decode(buf, st, en), full.decode(buf, st, en)
@@ -125,10 +126,11 @@ def test_device_view_confirms_an_optimistic_decode(monkeypatch):
         torch.cuda.synchronize(dev)
         on.decode_device(d_b.data_ptr(), buf.size, d_s.data_ptr(), d_e.data_ptr(), st.shape[0])
         cols = on.device_columns()
-        assert int(on.info().implicit_cols) == 3
+        assert int(on.info().implicit_cols) == 7
         n = st.shape[0]
         for name, dt, count, want in (("status", np.int32, n, np.array(ref.status)), ("verdict", np.uint8, n, np.array(ref.verdict)),
-                                      ("order", np.uint16, S * n, np.array(ref.order).reshape(-1))):
+                                      ("order", np.uint16, S * n, np.array(ref.order).reshape(-1)),
+                                      ("bytes_len", np.uint32, int(ref.info.kind_totals[1]), np.array(ref.bytes_len))):
             host = np.zeros(count, dt)
             p = ctypes.cast(getattr(cols, name), ctypes.c_void_p).value
             assert hip_rt.hipMemcpy(ctypes.c_void_p(host.ctypes.data), ctypes.c_void_p(p), ctypes.c_size_t(host.nbytes), 2) == 0
@@ -150,7 +152,7 @@ def test_optimistic_with_materialized_bytes_and_strict_crc(monkeypatch):
         buf, st, en = synth.framed(synth.c1_payloads(5000, offset=11))
         a = on.decode(buf, st, en, materialize_bytes=True)
         b = full.decode(buf, st, en, materialize_bytes=True)
-        assert int(a.info.implicit_cols) == 3 and on.device_bytes()[1] == 0
+        assert int(a.info.implicit_cols) == 3 and on.device_bytes()[1] == 0  # (lengths stored: the gather reads them)
         _same(a, b)
         assert np.array_equal(np.array(a.bytes_offsets), np.array(b.bytes_offsets))
         assert bytes(np.array(a.bytes_data)) == bytes(np.array(b.bytes_data))

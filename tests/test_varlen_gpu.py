@@ -45,6 +45,8 @@ def test_variable_length_ids_through_templates_vs_oracle():
         b = off.decode(buf, st, en)
         assert on.template_count() >= 16
         assert int(a.info.tpl_groups_missed) == 0, int(a.info.tpl_groups_missed)
+        # (ids of 5-12 bytes: no constant element length, the bytes_len column is stored)
+        assert not int(a.info.implicit_cols) & 4
         for k in COLS:
             assert np.array_equal(np.array(getattr(a, k)), np.array(getattr(b, k))), k
     finally:

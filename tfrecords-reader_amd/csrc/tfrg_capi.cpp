@@ -155,6 +155,8 @@ struct tfrg_ctx {
   bool no_quiet = false;      // (the re-run)
   bool opt_pending = false;   // the last decode ran optimistically and is not confirmed yet
   bool ord_const = false;     // (Learned::ord_const) of the learned shapes
+  bool len_const = false;     // (Learned::len_const)
+  std::vector<uint32_t> const_len;  // per slot: the bytes element length of every learned shape
   uint32_t last_implicit = 0; // TFRG_IMPLICIT_* columns the last decode did not store
   bool cols_complete = false; // tfrg_result_device filled them into the device columns
   bool mat_pending = false;   // an optimistic decode's byte materialization waits for its confirmation
@@ -570,6 +572,10 @@ struct Learned {
   bool have_spec = false;
   bool full = false;  // every sampled record took a kept template
   bool ord_const = false;  // every slot (< kLeanMaxSlots) at one key position in every kept template
+  // every bytes slot one element (mode 3) of one length in every kept template: an optimistic decode
+  // leaves the bytes_len column implicit (TFRG_IMPLICIT_BYTES_LEN); const_len[k] that length
+  bool len_const = false;
+  std::vector<uint32_t> const_len;
 };
 uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
                       const uint64_t* h_end, uint32_t n, uint32_t flags, Learned& out) {
@@ -761,6 +767,18 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
     out.ord_const = r0 != 0;
     for (uint32_t k = 1; out.ord_const && k < nt; ++k) out.ord_const = (w[(size_t)k * kLtWords + kLtSlot + 3 * s2] >> 16) == r0;
   }
+  out.len_const = S > 0 && S <= kLeanMaxSlots;
+  out.const_len.assign(S, 0u);
+  for (uint32_t s2 = 0; out.len_const && s2 < S; ++s2) {
+    if ((c->slot_kind[s2] & 3u) != TFRG_KIND_BYTES) continue;
+    const uint32_t z0 = w[kLtSlot + 3 * s2];
+    out.len_const = (z0 & 0xffu) == 3u && (z0 >> 16) != 0;
+    for (uint32_t k = 1; out.len_const && k < nt; ++k) {
+      const uint32_t zk = w[(size_t)k * kLtWords + kLtSlot + 3 * s2];
+      out.len_const = (zk & 0xffu) == 3u && (zk >> 16) != 0 && ((zk >> 8) & 0xffu) == ((z0 >> 8) & 0xffu);
+    }
+    out.const_len[s2] = (z0 >> 8) & 0xffu;
+  }
   out.w = std::move(w);
   out.spec = std::move(spec);
   out.img = std::move(img);
@@ -805,6 +823,8 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   c->have_spec = have_spec;
   c->tpl_full = L.full;
   c->ord_const = L.ord_const;
+  c->len_const = L.len_const;
+  c->const_len = L.const_len;
   return (int)nt;
 }
 
@@ -1062,6 +1082,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   cfg.optimistic = c->optimistic_on && !c->no_quiet && c->poison[0] == 0xffffffffu;
   cfg.ran_optimistic = false;
   cfg.ord_const = c->ord_const;
+  cfg.len_const = c->len_const && !mat;  // (the byte gather reads the lengths)
   cfg.implicit = 0;
   const uint64_t bound = c->call_bound ? c->call_bound : c->record_bound;
   c->call_bound = 0;
@@ -1237,6 +1258,20 @@ int tfrg_result_info(tfrg_ctx* c, tfrg_info* info) {
   return 0;
 }
 
+// (TFRG_IMPLICIT_BYTES_LEN) per bytes slot of an optimistic decode: its first row in the bytes
+// columns and its constant length. Every slot is placed, so slot k's rows are n * (its rank among
+// the bytes slots), as tpl_quiet_finish sets the column bases.
+static std::vector<std::pair<uint64_t, uint32_t>> implicit_len_runs(const tfrg_ctx* c) {
+  std::vector<std::pair<uint64_t, uint32_t>> out;
+  uint64_t base = 0;
+  for (uint32_t k = 0; k < c->n_slots; ++k) {
+    if ((c->slot_kind_h[k] & 3u) != TFRG_KIND_BYTES) continue;
+    out.push_back({base, k < c->const_len.size() ? c->const_len[k] : 0u});
+    base += c->n;
+  }
+  return out;
+}
+
 int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
   if (!c || !c->have_result) return TFRG_E_ARG;
   // an optimistic decode, or one whose value capacities were hinted below the worst case: confirmed
@@ -1274,6 +1309,10 @@ int tfrg_result_device(tfrg_ctx* c, tfrg_columns* d) {
       for (uint32_t k = 0; k < c->n_slots; ++k)
         HIP_TRY(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(c->order.as<uint16_t>() + (size_t)k * n),
                                   (unsigned short)(c->tpl_h[kLtSlot + 3 * k] >> 16), n, c->last_stream));
+    if (c->last_implicit & TFRG_IMPLICIT_BYTES_LEN)
+      for (const auto& [base, len] : implicit_len_runs(c))
+        HIP_TRY(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(c->b_len.as<uint32_t>() + base), (int)len, n,
+                                  c->last_stream));
   }
   c->cols_complete = true;
   d->status = c->status.as<int32_t>();
@@ -1341,7 +1380,11 @@ int tfrg_result_fetch(tfrg_ctx* c, const tfrg_columns* h) {
   HIP_TRY(cp(h->i64, c->i64.p, cl(info.kind_totals[TFRG_KIND_INT64], c->cap_i64) * 8));
   HIP_TRY(cp(h->f32, c->f32.p, cl(info.kind_totals[TFRG_KIND_FLOAT], c->cap_f32) * 4));
   HIP_TRY(cp(h->bytes_off, c->b_off.p, cl(info.kind_totals[TFRG_KIND_BYTES], c->cap_b) * 4));
-  HIP_TRY(cp(h->bytes_len, c->b_len.p, cl(info.kind_totals[TFRG_KIND_BYTES], c->cap_b) * 4));
+  if ((info.implicit_cols & TFRG_IMPLICIT_BYTES_LEN) && h->bytes_len) {
+    for (const auto& [base, len] : implicit_len_runs(c)) std::fill_n(h->bytes_len + base, n, len);
+  } else {
+    HIP_TRY(cp(h->bytes_len, c->b_len.p, cl(info.kind_totals[TFRG_KIND_BYTES], c->cap_b) * 4));
+  }
   if (c->materialized) {
     HIP_TRY(cp(h->bytes_data, c->bdata.p, info.bytes_data_len));
     HIP_TRY(cp(h->bytes_offsets, c->boff64.p, (info.kind_totals[TFRG_KIND_BYTES] + 1) * 8));

@@ -317,6 +317,7 @@ struct LaunchCfg {
   bool ran_optimistic;     // (out) this decode was launched optimistically: it is complete only once
                            // the host has read kInfoResid as 0 (else it is re-run in full)
   bool ord_const;          // every learned shape has every slot at the same key position
+  bool len_const;          // every bytes slot one element of one length in every learned shape
   uint32_t implicit;       // (out) TFRG_IMPLICIT_* columns the decode did not store
 };
 

@@ -3470,7 +3470,9 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     a.tsum = cfg.ran_optimistic ? nullptr : o.tsum;  // (placed slots: no scan; a re-run clears tsum)
     a.finish = cfg.ran_optimistic ? sc.slot_kind : nullptr;
     // (optimistic: status / verdict and constant order words are implicit, tfrg_info.implicit_cols)
-    cfg.implicit = cfg.ran_optimistic ? TFRG_IMPLICIT_STATUS | (cfg.ord_const ? TFRG_IMPLICIT_ORDER : 0u) : 0u;
+    cfg.implicit = cfg.ran_optimistic ? TFRG_IMPLICIT_STATUS | (cfg.ord_const ? TFRG_IMPLICIT_ORDER : 0u) |
+                                            (cfg.len_const ? TFRG_IMPLICIT_BYTES_LEN : 0u)
+                                      : 0u;
     a.implicit = cfg.implicit;
     a.n_slots = (uint32_t)S;
     a.tile_stride = o.tile_stride;

@@ -35,9 +35,6 @@ constexpr int kTplBlock = 512;        // 8 waves: the 32 KiB of tables are share
 constexpr uint32_t kTplTabs = 32;     // T_0 .. T_31
 static_assert(4u * kTplTabs * 256u + 4u * kLiMaxWords + 512u <= 65536u, "lane image + CRC tables exceed LDS");
 constexpr uint32_t kHitVerdict = TFRG_V_LEN_MATCH | TFRG_V_LEN_CRC | TFRG_V_DATA_CRC;
-#ifndef TFRG_TPL_GROUPS_PER_STEP
-#define TFRG_TPL_GROUPS_PER_STEP 1
-#endif
 
 typedef __attribute__((address_space(4))) const uint32_t cu32;  // wave-uniform reads -> s_load
 
@@ -139,11 +136,8 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     DevBatch B, DevOut o, LeanArgs A, const uint32_t* __restrict__ img, const uint32_t* __restrict__ tabs) {
   static_assert(W == 16 || W == 32 || W == 64, "window words");
   typedef uint32_t wvec __attribute__((ext_vector_type(W)));
-  __shared__ uint32_t tab[kTplTabs * 256];
+  __shared__ __attribute__((aligned(16))) uint32_t tab[kTplTabs * 256];
   extern __shared__ __attribute__((aligned(16))) uint32_t limg[];  // the templates' lane image
-  for (uint32_t i = threadIdx.x; i < kTplTabs * 256; i += kTplBlock) tab[i] = tabs[i];
-  for (uint32_t i = threadIdx.x; i < A.img_words; i += kTplBlock) limg[i] = img[i];
-  __syncthreads();
   constexpr uint32_t kWaves = kTplBlock / 64;
   constexpr uint32_t kTw = kLiTw(W);
   const uint32_t lane = threadIdx.x & 63u, wib = rfl(threadIdx.x >> 6);
@@ -310,8 +304,10 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
           }
         }
         if (mode == 3u) lx = en + pos;  // one bytes element: its batch offset and length
-        const uint32_t tot = (sq & kLiQSingle) ? (uint32_t)__popcll(__ballot(hit && cw != 0u))
-                                               : wave_sum(hit ? (cw & ~kCountInline) : 0u);
+        // (the tile sums: not kept by an optimistic decode, whose placed slots need no scan)
+        const uint32_t tot = !A.tsum ? 0u
+                             : (sq & kLiQSingle) ? (uint32_t)__popcll(__ballot(hit && cw != 0u))
+                                                 : wave_sum(hit ? (cw & ~kCountInline) : 0u);
         const LeanTgt& T = A.tg[k];
         if (hit) {
           if (!(A.implicit & TFRG_IMPLICIT_ORDER)) T.ord[r] = (uint16_t)(z.x >> 16);
@@ -322,7 +318,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
                 reinterpret_cast<uint64_t*>(T.v1)[r] = lx;
               } else {
                 reinterpret_cast<uint32_t*>(T.v1)[r] = lx;
-                if (T.kind == TFRG_KIND_BYTES) T.v2[r] = ly;
+                if (T.kind == TFRG_KIND_BYTES && !(A.implicit & TFRG_IMPLICIT_BYTES_LEN)) T.v2[r] = ly;
               }
             }
           } else {
@@ -351,38 +347,33 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
     }
     acc = 0;
   };
-#if TFRG_TPL_GROUPS_PER_STEP == 2
-  // two groups per step, their windows loaded together: a step waits once, for both windows and
-  // the previous step's column stores (gfx9 counts stores in vmcnt, in issue order), so each wait
-  // covers 128 records; the next step's offsets are requested before this step's stores
-  LaneOff f0 = offsets(gbeg), f1 = offsets(gbeg + 1u);
-  for (uint32_t g = gbeg; g < gend; g += 2u) {
-    wvec wa, wb;
-    window(wa, f0, g);
-    window(wb, f1, g + 1u);
-    const LaneOff fa = f0, fb = f1;
-    f0 = offsets(g + 2u);
-    f1 = offsets(g + 3u);
-    proc(wa, g, fa);
-    if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);  // (gpw 2 / a batch's last group)
-    if (g + 1u < gend) {
-      proc(wb, g + 1u, fb);
-      if (((g + 2u) & 3u) == 0u || g + 2u >= gend) flush(g + 1u);
-    }
-  }
-#else
   // one group per step (one window live: the per-lane template words need the registers); the next
-  // group's offsets are requested before this group's stores
+  // group's offsets are requested before this group's stores. The wave's first offsets and window
+  // are requested before the workgroup copies its CRC tables and lane image into LDS, so its first
+  // HBM round trips overlap that copy (~3 % of a launch of 2,000 workgroups).
   LaneOff f0 = offsets(gbeg);
+  static_assert(kTplTabs * 256u % (4u * kTplBlock) == 0u, "table copy in whole 16-byte rounds");
+  constexpr uint32_t kTabRounds = kTplTabs * 256u / (4u * kTplBlock);
+  u32x4 tv[kTabRounds];
+#pragma unroll
+  for (uint32_t j = 0; j < kTabRounds; ++j) tv[j] = reinterpret_cast<const u32x4*>(tabs)[threadIdx.x + j * kTplBlock];
+  wvec wa;
+  window(wa, f0, gbeg);
+  LaneOff fa = f0;
+  f0 = offsets(gbeg + 1u);
+#pragma unroll
+  for (uint32_t j = 0; j < kTabRounds; ++j) reinterpret_cast<u32x4*>(tab)[threadIdx.x + j * kTplBlock] = tv[j];
+  for (uint32_t i = threadIdx.x; i < A.img_words; i += kTplBlock) limg[i] = img[i];
+  __syncthreads();
   for (uint32_t g = gbeg; g < gend; ++g) {
-    wvec wa;
-    window(wa, f0, g);
-    const LaneOff fa = f0;
-    f0 = offsets(g + 1u);
     proc(wa, g, fa);
     if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);
+    if (g + 1u < gend) {
+      window(wa, f0, g + 1u);
+      fa = f0;
+      f0 = offsets(g + 2u);
+    }
   }
-#endif
   if (A.finish) {  // (uniform) optimistic decode: the last workgroup to finish ends it
     __shared__ uint32_t s_listed[kWaves];
     __shared__ uint32_t s_last, s_total;

@@ -96,6 +96,15 @@ VARIANTS = {
                   "  pmask = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(pmask >> 32)) << 32) | __builtin_amdgcn_readfirstlane((uint32_t)pmask);\n")],
     # k_tpl_lane without the status / verdict stores (wrong results)
     "nostatus": [("tfrg_tpl.hip", "        o.status[r] = TFRG_OK;\n        o.verdict[r] = (uint8_t)kHitVerdict;\n", "")],
+    # k_tpl_lane ablations (round 6; timing only, wrong results): no payload CRC / no template
+    # match / no slot extraction and column stores / none of the three
+    "abl_nocrc": [('tfrg_tpl.hip', '      if (chain_u < (uint32_t)(W - 9)) {', '      if (false) {'), ('tfrg_tpl.hip', '      TFRG_LIN(0) TFRG_LIN(1) TFRG_LIN(2) TFRG_LIN(3) TFRG_LIN(4) TFRG_LIN(5) TFRG_LIN(6) TFRG_LIN(7)\n', ''), ('tfrg_tpl.hip', '      const bool ok = act && diff == 0u && crc_mask(lin ^ meta.y) == w[W - 1];', '      const bool ok = act && diff == 0u && (lin | meta.y | w[W - 1] | c | 1u) != 0u;')],
+    "abl_nomatch": [('tfrg_tpl.hip', '        diff |= ((w[4 * q] ^ bm.x) & mm.x) | ((w[4 * q + 1] ^ bm.y) & mm.y) | ((w[4 * q + 2] ^ bm.z) & mm.z) |\n                ((w[4 * q + 3] ^ bm.w) & mm.w);', '        diff |= 0u * (bm.x & mm.x);')],
+    "abl_noslot": [('tfrg_tpl.hip', '    if (__ballot(hit)) {\n      const uint32_t* ts', '    if (__ballot(hit) && A.n_slots == 12345u) {\n      const uint32_t* ts')],
+    "abl_none": [('tfrg_tpl.hip', '      if (chain_u < (uint32_t)(W - 9)) {', '      if (false) {'), ('tfrg_tpl.hip', '      TFRG_LIN(0) TFRG_LIN(1) TFRG_LIN(2) TFRG_LIN(3) TFRG_LIN(4) TFRG_LIN(5) TFRG_LIN(6) TFRG_LIN(7)\n', ''), ('tfrg_tpl.hip', '      const bool ok = act && diff == 0u && crc_mask(lin ^ meta.y) == w[W - 1];', '      const bool ok = act && diff == 0u && (lin | meta.y | w[W - 1] | c | 1u) != 0u;'), ('tfrg_tpl.hip', '        diff |= ((w[4 * q] ^ bm.x) & mm.x) | ((w[4 * q + 1] ^ bm.y) & mm.y) | ((w[4 * q + 2] ^ bm.z) & mm.z) |\n                ((w[4 * q + 3] ^ bm.w) & mm.w);', '        diff |= 0u * (bm.x & mm.x);'), ('tfrg_tpl.hip', '    if (__ballot(hit)) {\n      const uint32_t* ts', '    if (__ballot(hit) && A.n_slots == 12345u) {\n      const uint32_t* ts')],
+    # k_tpl_lane: 16 / 32 groups per wave on large batches (fewer workgroups, fewer table copies)
+    "gpw16": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 16u * (uint32_t)num_cus ? 16u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw >= 8u) {')],
+    "gpw32": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 32u * (uint32_t)num_cus ? 32u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw >= 8u) {')],
 }
 
 
