@@ -1385,25 +1385,6 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   lds_u32* tsl = (lds_u32*)(krec + sc.n_keys * kKrWords) + wib * 64u;  // MODE 1: this wave's tile sums
   uint32_t* spec_l = krec + sc.n_keys * kKrWords + (MODE == 1 ? kWaves * 64u : 0u);  // MODE 0: DevSchema::spec
   uint32_t* spec_tl = spec_l + ((S + 7u) & ~7u);  // MODE 0: its targets (16-byte aligned)
-  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneCountBlock) tab[i] = crc_tab[2048 + i / R];
-  if constexpr (MODE == 1) {
-    tsl[lane] = 0;
-  }
-  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
-  if (fast_ok) {
-    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneCountBlock) kht[i] = sc.ht[i];
-    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneCountBlock) krec[i] = sc.krec[i];
-  }
-  const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
-  if (spec_on)
-    for (uint32_t i = threadIdx.x; i < S; i += kLaneCountBlock) {
-      spec_l[i] = sc.spec[i];
-      spec_target(spec_tl + kSpecTgtWords * i, o, sc.spec[i], B.n);
-    }
-  __syncthreads();
-  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
-  const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
-
   // 64-record groups: group g of the batch, or (residual mode) the g-th listed group with its mask
   const uint32_t nw = gridDim.x * kWaves;
   auto group = [&](uint32_t g, uint64_t& gb, uint64_t& gm) -> bool {
@@ -1422,12 +1403,32 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
   uint64_t base = 0, gmask = 0;
   bool more = group(g, base, gmask);
   // the next group's offsets are requested before this group's stores (one HBM round trip less on
-  // the critical path of the next group)
+  // the critical path of the next group); the first group's before the workgroup's table copy, so
+  // that its round trip overlaps the copy
   uint64_t nst = 0, nen = 0;
   if (more && base + lane < B.n) {
     nst = rec_start(B, (uint32_t)(base + lane));
     nen = rec_end(B, (uint32_t)(base + lane));
   }
+
+  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice * R; i += kLaneCountBlock) tab[i] = crc_tab[2048 + i / R];
+  if constexpr (MODE == 1) {
+    tsl[lane] = 0;
+  }
+  const bool fast_ok = sc.n_keys <= kLdsMaxKeys && sc.ht_mask + 1 <= kLdsMaxHt;  // else every record is slow
+  if (fast_ok) {
+    for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += kLaneCountBlock) kht[i] = sc.ht[i];
+    for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += kLaneCountBlock) krec[i] = sc.krec[i];
+  }
+  const bool spec_on = MODE == 0 && fast_ok && sc.spec != nullptr;
+  if (spec_on)
+    for (uint32_t i = threadIdx.x; i < S; i += kLaneCountBlock) {
+      spec_l[i] = sc.spec[i];
+      spec_target(spec_tl + kSpecTgtWords * i, o, sc.spec[i], B.n);
+    }
+  __syncthreads();
+  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
+  const LdsTab<R> T{tab, threadIdx.x & (R - 1)};
   while (more) {
     PHASE_MARK(p0);
     const uint64_t ri = base + lane;
@@ -2096,15 +2097,20 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   uint32_t* A1 = lds;           // [4][256] (x) x^8192, then (x) x^16384, (x) x^32768
   uint32_t* rot = lds + 3072;   // [256][64] rotated slice-by-16 (chunk_rot)
   uint32_t* cst = lds + 19456;  // [kNumCst]
-  for (uint32_t i = threadIdx.x; i < 1024u; i += BLK) A1[i] = crc_tab[1024 + i];
-  for (uint32_t i = threadIdx.x; i < 2048u; i += BLK) A1[1024 + i] = crc_tab[24576 + i];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(crc_tab + 8192);
-    uint4* dst = reinterpret_cast<uint4*>(rot);
-    for (uint32_t i = threadIdx.x; i < 4096u; i += BLK) dst[i] = src[i];
+  // the 77 KiB of tables are loaded into registers first and written to LDS only after this wave's
+  // search for its first list entry and its window load: those dependent HBM round trips overlap
+  // the table loads instead of following them (every wave of the launch starts with them)
+  static_assert(3072u % BLK == 0u && 4096u % BLK == 0u && kNumCst <= BLK, "table copy shape");
+  uint32_t ta[3072u / BLK];
+  uint4 tr[4096u / BLK];
+#pragma unroll
+  for (uint32_t j = 0; j < 3072u / BLK; ++j) {
+    const uint32_t i = j * BLK + threadIdx.x;
+    ta[j] = i < 1024u ? crc_tab[1024 + i] : crc_tab[24576 + (i - 1024u)];
   }
-  for (uint32_t i = threadIdx.x; i < kNumCst; i += BLK) cst[i] = consts[i];
-  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < 4096u / BLK; ++j) tr[j] = reinterpret_cast<const uint4*>(crc_tab + 8192)[j * BLK + threadIdx.x];
+  const uint32_t tc = threadIdx.x < kNumCst ? consts[threadIdx.x] : 0u;
   const RotTabView T{reinterpret_cast<const uint8_t*>(lds)};
   const bool tab_at0 = (uint32_t)(uintptr_t)lds == 0u;  // (the asm chunk path addresses LDS 0)
   // the batch's readable bytes (round_up(nbytes, 16), at most 2^32 - 1: batches are < 4 GiB) as a
@@ -2117,10 +2123,10 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   const CrcRot RR = crc_rot_init(lane);
   const uint64_t W = (uint64_t)gridDim.x * (BLK / 64), wv = (uint64_t)blockIdx.x * (BLK / 64) + wib;
   const uint64_t R0 = TR * wv / W, R1 = TR * (wv + 1) / W;
-  if (R0 >= R1) return;  // (wave-uniform; no barrier follows)
+  const bool work = R0 < R1;  // (wave-uniform)
   PHASE_MARK(q0);
   // the list entry holding flat round R0: 64-ary search over the ascending bases
-  uint32_t lo = 0, hi = nrec;  // base[lo] <= R0 < base[hi] (base[nrec] = TR)
+  uint32_t lo = 0, hi = work ? nrec : 1u;  // base[lo] <= R0 < base[hi] (base[nrec] = TR)
   while (hi - lo > 1u) {
     const uint32_t step = (hi - lo + 63u) >> 6;
     const uint32_t k = lo + lane * step;
@@ -2129,7 +2135,15 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
     hi = rfl32(lo + step < hi ? lo + step : hi);
   }
   uint32_t win0 = lo;
-  CrcWin w = crc_win_load(B, o, win0, nrec, TR, lane);
+  CrcWin w{};
+  if (work) w = crc_win_load(B, o, win0, nrec, TR, lane);
+#pragma unroll
+  for (uint32_t j = 0; j < 3072u / BLK; ++j) A1[j * BLK + threadIdx.x] = ta[j];
+#pragma unroll
+  for (uint32_t j = 0; j < 4096u / BLK; ++j) reinterpret_cast<uint4*>(rot)[j * BLK + threadIdx.x] = tr[j];
+  if (threadIdx.x < kNumCst) cst[threadIdx.x] = tc;
+  __syncthreads();
+  if (!work) return;  // (no barrier follows)
   uint64_t lim = rl64(w.base, 63);
   lim = lim < R1 ? lim : R1;
   PHASE_MARK(q1);

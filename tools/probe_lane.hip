@@ -38,7 +38,9 @@ struct Cols {
 };
 
 enum : int { kU64 = 1, kStore = 2, kPipe = 4, kCheck = 8, kNoSV = 16, kNoOrd = 32, kStaged = 64, kTabLds = 128,
-             kTab8 = 256 };
+             kTab8 = 256, kGlds = 512, kTab16 = 1024, kNoLen = 2048 };
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
 
 template <int MODE>
 __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t nbytes, const uint64_t* st64,
@@ -73,7 +75,7 @@ __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t
   };
   __shared__ __attribute__((aligned(16))) uint32_t stage[8][1024 + 32];  // 4 KiB + slack per wave
   // kTabLds: 32 KiB more LDS per workgroup (k_tpl_lane's CRC position tables): 2 workgroups per CU
-  constexpr uint32_t kPad = (MODE & kTabLds) ? ((MODE & kTab8) ? 2048u : 8192u) : 1u;
+  constexpr uint32_t kPad = (MODE & kTabLds) ? ((MODE & kTab8) ? 2048u : (MODE & kTab16) ? 4096u : 8192u) : 1u;
   __shared__ uint32_t tabpad[kPad];
   if (MODE & kTabLds) {
     for (uint32_t i = threadIdx.x; i < kPad; i += 512u) tabpad[i] = i;
@@ -137,11 +139,47 @@ __global__ __launch_bounds__(512, 6) void k_probe(const uint8_t* bytes, uint32_t
         }
         c.v[r] = w[10] & 0x7fu;
         c.boff[r] = e - 16u;
-        c.blen[r] = 12u;
+        if (!(MODE & kNoLen)) c.blen[r] = 12u;
       }
     }
   };
-  if (MODE & kPipe) {
+  if (MODE & kGlds) {
+    // round 6: each wave's next window loaded straight into its LDS buffer (global_load_lds, lane-
+    // linear: lane l's 16-byte piece q at q * 1 KiB + 16 l) while this group is processed from VGPRs
+    auto issue = [&](uint32_t e) {
+      const uint32_t voff = e >= 64u ? e - 64u : 0u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        __builtin_amdgcn_global_load_lds((gvoid*)(bytes + voff + 16u * q), (lvoid*)(st_w + 256u * q), 16, 0, 0);
+    };
+    uint32_t sa, ea, sb = 0, eb = 0;
+    ends(g0, sa, ea);
+    issue(ea);
+    if (g0 + 1u < g1) ends(g0 + 1u, sb, eb);
+    for (uint32_t g = g0; g < g1; ++g) {
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      asm volatile("" ::: "memory");
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(st_w + 256u * q + 4u * lane);
+        w[4 * q] = v.x;
+        w[4 * q + 1] = v.y;
+        w[4 * q + 2] = v.z;
+        w[4 * q + 3] = v.w;
+      }
+      __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the buffer is read before it is refilled
+      asm volatile("" ::: "memory");
+      const uint32_t s_ = sa, e_ = ea;
+      if (g + 1u < g1) {
+        issue(eb);
+        sa = sb;
+        ea = eb;
+        if (g + 2u < g1) ends(g + 2u, sb, eb);
+      }
+      proc(g, s_, e_, w);
+    }
+  } else if (MODE & kPipe) {
     uint32_t sa, ea, sb, eb;
     uint32_t wa[16];
     ends(g0, sa, ea);
@@ -243,13 +281,25 @@ int main(int argc, char** argv) {
   printf("{\"records\": %u, \"bytes\": %u}\n", n, nb);
   auto rep_ = [&](const char* name, int mode, uint32_t tpw, float ms) {
     const double rd = (double)nb + (mode & kU64 ? 16.0 : 4.0) * n;
-    const double wr = mode & kStore ? (25.0 - (mode & kNoSV ? 5.0 : 0.0) - (mode & kNoOrd ? 4.0 : 0.0)) * n : 0.0;
+    const double wr = mode & kStore ? (25.0 - (mode & kNoSV ? 5.0 : 0.0) - (mode & kNoOrd ? 4.0 : 0.0) -
+                                       (mode & kNoLen ? 4.0 : 0.0)) * n : 0.0;
     printf("{\"variant\": \"%s\", \"tiles_per_wave\": %u, \"ms\": %.4f, \"alg_TBps\": %.3f, \"frac\": %.4f, "
            "\"framed_GiBps\": %.1f}\n",
            name, tpw, ms, (rd + wr) / ms / 1e9, (rd + wr) / ms / 1e9 / 8.0, nb / (ms / 1e3) / 1073741824.0);
     fflush(stdout);
   };
   for (int rep = 0; rep < 2; ++rep)
+    for (uint32_t tpw : {1u, 2u}) {
+      constexpr int V = kStore | kNoSV | kNoOrd | kNoLen;
+      rep_("v12_lane", V, tpw, run<V>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("v12_lane_tab", V | kTabLds, tpw, run<V | kTabLds>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("v12_glds_tab16", V | kGlds | kTabLds | kTab16, tpw,
+           run<V | kGlds | kTabLds | kTab16>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("v12_glds", V | kGlds, tpw, run<V | kGlds>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("read_glds", kGlds, tpw, run<kGlds>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+      rep_("read_lane", 0, tpw, run<0>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
+    }
+  for (int rep = 0; rep < 0; ++rep)
     for (uint32_t tpw : {1u}) {
       rep_("rw_u32_tab", kStore | kTabLds, tpw, run<kStore | kTabLds>(d_b, nb, d_s64, d_e64, d_e32, n, c, tpw, reps));
       rep_("rw_u32_staged_tab8", kStore | kStaged | kTabLds | kTab8, tpw,

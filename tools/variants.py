@@ -105,6 +105,10 @@ VARIANTS = {
     # k_tpl_lane: 16 / 32 groups per wave on large batches (fewer workgroups, fewer table copies)
     "gpw16": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 16u * (uint32_t)num_cus ? 16u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw >= 8u) {')],
     "gpw32": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 32u * (uint32_t)num_cus ? 32u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw >= 8u) {')],
+    # k_tpl_lane on large batches: {3, 6} workgroups per CU in all, each wave one contiguous run of
+    # groups (a table copy per resident workgroup, not per 64 groups)
+    "persist3": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? ((groups + 3u * (uint32_t)num_cus * 8u - 1u) / (3u * (uint32_t)num_cus * 8u) + 3u) & ~3u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw == 0xfffu) {')],
+    "persist6": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? ((groups + 6u * (uint32_t)num_cus * 8u - 1u) / (6u * (uint32_t)num_cus * 8u) + 3u) & ~3u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw == 0xfffu) {')],
 }
 
 
