@@ -34,15 +34,18 @@ def main() -> None:
     batches = int(line["config"]["batches_per_gpu"])
     rows = list(csv.DictReader(open(next(out.rglob("*kernel_trace.csv")))))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    # the timed steps are the first decodes after bench.py's marker kernel (k_stream_read over 16
+    # bytes, bench._mark): the learning sample and the warmup come before it, the consumer and
+    # profiling steps after the timed ones
+    mark = next((i for i, r in enumerate(rows) if "k_stream_read" in r["Kernel_Name"]), -1)
     per = defaultdict(list)
-    for r in rows:
+    for r in rows[mark + 1 :]:
         name = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
         base = next((k for k in DECODE if k in name), None)
         if base:
             per[base].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
-    # (the last decode of each batch is bench.py's profiling step, with HIP events: dropped)
     k = steps * batches
-    us = {name: sum(d[-k - batches : -batches]) / steps for name, d in per.items() if len(d) >= k + batches}
+    us = {name: sum(d[:k]) / steps for name, d in per.items() if len(d) >= k}
     res = {"only": only, "workload": line["config"]["workload"], "records": line["config"]["records_per_gpu"],
            "steps": steps, "batches": batches, "kernels_us_per_step": {n: round(v, 2) for n, v in us.items()},
            "kernels_sum_us": round(sum(us.values()), 2), "bench_ms_per_step": line["ms_per_step"]}

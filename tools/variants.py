@@ -109,6 +109,9 @@ VARIANTS = {
     # groups (a table copy per resident workgroup, not per 64 groups)
     "persist3": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? ((groups + 3u * (uint32_t)num_cus * 8u - 1u) / (3u * (uint32_t)num_cus * 8u) + 3u) & ~3u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw == 0xfffu) {')],
     "persist6": [('tfrg_tpl.hip', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? 8u : 4u;', 'a2.gpw = need < (uint32_t)num_cus / 2u ? 1u : need < (uint32_t)num_cus ? 2u : need >= 8u * (uint32_t)num_cus ? ((groups + 6u * (uint32_t)num_cus * 8u - 1u) / (6u * (uint32_t)num_cus * 8u) + 3u) & ~3u : 4u;'), ('tfrg_tpl.hip', 'if (split_on && a2.gpw == 8u) {', 'if (split_on && a2.gpw == 0xfffu) {')],
+    # k_tpl_lane at 7 waves/SIMD (72 VGPRs)
+    "lb7": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
+             "__launch_bounds__(kTplBlock, W == 16 ? 7 : (W == 32 ? 4 : 2))")],
 }
 
 
