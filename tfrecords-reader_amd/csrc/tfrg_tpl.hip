@@ -185,7 +185,7 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   auto in_batch = [&](uint32_t g, uint32_t s, uint32_t e) {
     return (g << 6) + lane < B.n && s <= e && e <= nb && e >= 16u;
   };
-  auto window = [&](wvec& wn, const LaneOff& f, uint32_t g) {
+  auto window = [&](wvec& wn, const LaneOff& f) {
     const uint32_t e = f.e;
     const bool full = e >= 4u * W && e <= nb;
     const uint32_t voff = full ? e - 4u * W : 0xffffff00u;
@@ -197,21 +197,26 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
       wn[4 * q + 2] = v.z;
       wn[4 * q + 3] = v.w;
     }
-    // a record ending in the batch's first 4 W bytes (group 0 only): its window begins before the
-    // batch; those bytes are outside the record (template mask 0), the rest is read byte by byte
-    if (g == 0u) {
-      const bool head = in_batch(g, start_of(f), e) && !full;
-      if (__ballot(head)) {
+  };
+  // a record ending in the batch's first 4 W bytes (group 0 only): its window begins before the
+  // batch; those bytes are outside the record (template mask 0), the rest is read byte by byte. (Its
+  // own step, after the prologue: byte loads pending at a merge with the common path made the
+  // compiler wait for every load in flight there.)
+  auto head_fix = [&](wvec& wn, const LaneOff& f, uint32_t g) {
+    if (g != 0u) return;  // (uniform)
+    const uint32_t e = f.e;
+    const bool full = e >= 4u * W && e <= nb;
+    const bool head = in_batch(g, start_of(f), e) && !full;
+    if (__ballot(head)) {
 #pragma unroll
-        for (int i = 0; i < W; ++i) {
-          uint32_t x = 0;
+      for (int i = 0; i < W; ++i) {
+        uint32_t x = 0;
 #pragma unroll
-          for (int b = 0; b < 4; ++b) {
-            const int64_t p = (int64_t)e - 4 * W + 4 * i + b;
-            if (head && p >= 0) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0) << (8 * b);
-          }
-          if (head) wn[i] = x;
+        for (int b = 0; b < 4; ++b) {
+          const int64_t p = (int64_t)e - 4 * W + 4 * i + b;
+          if (head && p >= 0) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, (uint32_t)p, 0, 0) << (8 * b);
         }
+        if (head) wn[i] = x;
       }
     }
   };
@@ -351,25 +356,28 @@ __global__ __launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2)) void k_
   // group's offsets are requested before this group's stores. The wave's first offsets and window
   // are requested before the workgroup copies its CRC tables and lane image into LDS, so its first
   // HBM round trips overlap that copy (~3 % of a launch of 2,000 workgroups).
-  LaneOff f0 = offsets(gbeg);
+  // (the first round of the table and image copies, the first two groups' offsets: all in flight
+  // together; then the first window, which needs the offsets)
+  LaneOff fa = offsets(gbeg), f0 = offsets(gbeg + 1u);
   static_assert(kTplTabs * 256u % (4u * kTplBlock) == 0u, "table copy in whole 16-byte rounds");
   constexpr uint32_t kTabRounds = kTplTabs * 256u / (4u * kTplBlock);
   u32x4 tv[kTabRounds];
 #pragma unroll
   for (uint32_t j = 0; j < kTabRounds; ++j) tv[j] = reinterpret_cast<const u32x4*>(tabs)[threadIdx.x + j * kTplBlock];
+  const uint32_t iw0 = threadIdx.x < A.img_words ? img[threadIdx.x] : 0u;
   wvec wa;
-  window(wa, f0, gbeg);
-  LaneOff fa = f0;
-  f0 = offsets(gbeg + 1u);
+  window(wa, fa);
 #pragma unroll
   for (uint32_t j = 0; j < kTabRounds; ++j) reinterpret_cast<u32x4*>(tab)[threadIdx.x + j * kTplBlock] = tv[j];
-  for (uint32_t i = threadIdx.x; i < A.img_words; i += kTplBlock) limg[i] = img[i];
+  if (threadIdx.x < A.img_words) limg[threadIdx.x] = iw0;
+  for (uint32_t i = threadIdx.x + kTplBlock; i < A.img_words; i += kTplBlock) limg[i] = img[i];
   __syncthreads();
   for (uint32_t g = gbeg; g < gend; ++g) {
+    head_fix(wa, fa, g);
     proc(wa, g, fa);
     if (((g + 1u) & 3u) == 0u || g + 1u >= gend) flush(g);
     if (g + 1u < gend) {
-      window(wa, f0, g + 1u);
+      window(wa, f0);
       fa = f0;
       f0 = offsets(g + 2u);
     }
