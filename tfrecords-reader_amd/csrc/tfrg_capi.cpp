@@ -440,7 +440,8 @@ static DevSchema schema_view(const tfrg_ctx* c) {
   // speculative placement is a property of the learned shapes' schema (a slot that is one inline
   // value in every shape), not of the template match: it stays on with the templates off, where
   // k_lane_count places those values itself
-  s.spec = c->spec_on && c->have_spec && c->n_tpl ? c->spec.as<uint32_t>() : nullptr;
+  // (and without any shape: learn_single_slots)
+  s.spec = c->spec_on && c->have_spec ? c->spec.as<uint32_t>() : nullptr;
   return s;
 }
 
@@ -787,6 +788,65 @@ uint32_t learn_shapes(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, ui
   return nt;
 }
 
+// Speculative placement without record shapes (records too large or too varied for a template,
+// C2's flowers): a slot whose list is one inline value -- one bytes element, one float, one int64
+// varint of <= 4 bytes (k_lane_count's inline rule) -- in every record of the sample that decodes,
+// by the host decoder (the reference's semantics). Ranks per kind in slot order up to the first slot
+// of that kind that is not one (as learn_shapes). Returns whether any slot was placed.
+bool learn_single_slots(const TplSchema* c, uint32_t S, const uint8_t* h_bytes, uint64_t nbytes,
+                        const uint64_t* h_start, const uint64_t* h_end, uint32_t n, uint32_t flags,
+                        std::vector<uint32_t>& spec) {
+  spec.assign(S ? S : 1, 0u);
+  if (!S || !n) return false;
+  tfrg_host_ctx* hc = nullptr;
+  if (tfrg_host_ctx_create(&hc)) return false;
+  std::vector<uint32_t> single(S, 0u);
+  uint32_t m = 0;
+  const uint32_t lim = n < 4096u ? n : 4096u;
+  for (uint32_t j = 0; j < lim; ++j) {
+    const uint32_t i = (uint32_t)((uint64_t)j * n / lim);
+    uint64_t a = h_start[i], e = h_end[i];
+    if (e > nbytes || e < a) continue;
+    if (!(flags & TFRG_FLAG_PAYLOAD_ONLY)) {
+      if (e - a < 16) continue;
+      a += 12;
+      e -= 4;
+    }
+    tfrg_host_record rec;
+    if (tfrg_host_decode(hc, h_bytes + a, e - a, flags, &rec) || rec.status != TFRG_OK) continue;
+    ++m;
+    for (uint32_t k = 0; k < rec.n_entries; ++k) {
+      const auto it = c->key_id.find(std::string((const char*)h_bytes + a + rec.key_off[k], rec.key_len[k]));
+      if (it == c->key_id.end()) continue;
+      const uint32_t kind = rec.kind[k];
+      if (kind < 1 || kind > 3) continue;
+      const int32_t slot = c->key_slot[4ull * it->second + kind];
+      if (slot < 0 || (uint32_t)slot >= S || rec.val_cnt[k] != 1) continue;
+      if (kind == TFRG_KIND_INT64) {
+        const int64_t v = rec.i64[rec.val_off[k]];
+        if (v < 0 || v >= (int64_t)1 << 28) continue;  // (more than 4 varint bytes: not inline)
+      }
+      ++single[slot];
+    }
+  }
+  tfrg_host_ctx_destroy(hc);
+  if (!m) return false;
+  bool any = false;
+  uint32_t rank[4] = {0, 0, 0, 0};
+  bool open[4] = {true, true, true, true};
+  for (uint32_t k = 0; k < S; ++k) {
+    const uint32_t kd = c->slot_kind[k] & 3u;
+    if (!open[kd]) continue;
+    if (single[k] == m) {
+      spec[k] = ((++rank[kd]) << 2) | kd;
+      any = true;
+    } else {
+      open[kd] = false;
+    }
+  }
+  return any;
+}
+
 }  // namespace
 
 extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const uint64_t* h_start,
@@ -799,7 +859,20 @@ extern "C" int tfrg_learn_templates(tfrg_ctx* c, const uint8_t* h_bytes, uint64_
   const TplSchema sch{c->key_id, c->key_slot_h, c->slot_kind_h};
   Learned L;
   const uint32_t nt = learn_shapes(&sch, c->n_slots, h_bytes, nbytes, h_start, h_end, n, flags, L);
-  if (!nt) return 0;
+  if (!nt) {  // no record shape: the speculative placement of single-value slots alone
+    std::vector<uint32_t> spec;
+    if (!learn_single_slots(&sch, c->n_slots, h_bytes, nbytes, h_start, h_end, n, flags, spec)) return 0;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->last_stream) HIP_TRY(hipStreamSynchronize(c->last_stream));
+    if (c->spec.ensure((size_t)c->n_slots * 4)) {
+      set_error("template allocation failed");
+      return TFRG_E_NOMEM;
+    }
+    HIP_TRY(hipMemcpy(c->spec.p, spec.data(), (size_t)c->n_slots * 4, hipMemcpyHostToDevice));
+    c->spec_h = spec;
+    c->have_spec = true;
+    return 0;
+  }
   const uint32_t S = c->n_slots;
   const std::vector<uint32_t>& w = L.w;
   const bool have_spec = L.have_spec;
@@ -1081,6 +1154,7 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   // (the poison hook needs the gathers it tests)
   cfg.optimistic = c->optimistic_on && !c->no_quiet && c->poison[0] == 0xffffffffu;
   cfg.ran_optimistic = false;
+  cfg.ran_quiet_big = false;
   cfg.ord_const = c->ord_const;
   cfg.len_const = c->len_const && !mat;  // (the byte gather reads the lengths)
   cfg.implicit = 0;
@@ -1143,6 +1217,9 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   c->have_result = true;
   c->rs_complete = false;
   c->opt_pending = n != 0 && cfg.ran_optimistic;
+  // (an optimistic decode without shapes leaves the lane kernel's tile sums in the scan words: the
+  // next decode clears them; one with shapes writes none)
+  if (n != 0 && cfg.ran_quiet_big) c->tsum_dirty = true;
   c->mat_pending = c->opt_pending && mat && S;
   c->last_implicit = n != 0 ? cfg.implicit : 0u;
   c->cols_complete = false;

@@ -318,6 +318,7 @@ struct LaunchCfg {
                            // the host has read kInfoResid as 0 (else it is re-run in full)
   bool ord_const;          // every learned shape has every slot at the same key position
   bool len_const;          // every bytes slot one element of one length in every learned shape
+  bool ran_quiet_big;      // (out) optimistic without shapes: k_tail_count's last workgroup ends it
   uint32_t implicit;       // (out) TFRG_IMPLICIT_* columns the decode did not store
 };
 

@@ -2319,13 +2319,70 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
 // ms; its own launch cost every batch ~6.5 us.)
 // 512-thread blocks: the streaming CRC's 70 KiB of LDS tables then still leave 4 waves per SIMD.
 constexpr uint32_t kTailBlock = 512;
+constexpr uint32_t kTailFinishWord = 19456 + kNumCst;  // two LDS words of the finishing workgroup
+
+// The end of an optimistic decode without record shapes (launch_all, `finish`: every slot placed
+// speculatively, records above lane_max possible), by the last workgroup of k_tail_count. When the
+// lane kernel placed every record's every slot (no irregular record, irr[k] = 0), sent none to the
+// exact walker, missed no key and listed no record for the wave gathers, the passes after this one
+// (k_spine, k_down_gather, k_tail_gather) would only do their bookkeeping: done here, as
+// tpl_quiet_finish does for k_tpl_lane. Anything else: kInfoResid = 1 and the host re-runs the
+// decode with every pass (tfrg_result_info). (The tile sums the lane kernel wrote are cleared by the
+// host before the next decode.)
+// (s_ok: a word of the dynamic LDS; a static __shared__ object would move the dynamic region off LDS
+// address 0, which role 2's table lookups address directly)
+__device__ void tail_quiet_finish(const DevOut& o, const uint8_t* slot_kind, uint32_t n_slots, uint32_t n,
+                                  volatile uint32_t& s_ok) {
+  if (threadIdx.x == 0) {
+    s_ok = o.info[kInfoSlow] == 0u && o.info[kInfoMissRecords] == 0u && o.info[kInfoErrors] == 0u &&
+           o.info[kInfoBig] == 0u && o.info[kInfoHuge] == 0u && o.info[kInfoDefer] == 0u;
+  }
+  __syncthreads();
+  if (threadIdx.x < n_slots && o.irr[threadIdx.x] != 0u) s_ok = 0u;  // (benign race: only zeroes)
+  for (uint32_t k = threadIdx.x + kTailBlock; k < n_slots; k += kTailBlock)
+    if (o.irr[k] != 0u) s_ok = 0u;
+  __syncthreads();
+  if (!s_ok) {
+    if (threadIdx.x == 0) o.info[kInfoResid] = 1u;
+    return;
+  }
+  for (uint32_t k = threadIdx.x; k < n_slots; k += kTailBlock) {
+    o.totals[k] = n;
+    o.rs[(size_t)k * (n + 1u) + n] = n;
+  }
+  if (threadIdx.x == 0) {
+    uint64_t acc[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < n_slots; ++k) {
+      const uint32_t kd = slot_kind[k] & 3u;
+      o.slot_base[k] = acc[kd];
+      acc[kd] += n;
+    }
+    for (int k = 0; k < 4; ++k) o.kind_totals[k] = acc[k];
+    if (acc[TFRG_KIND_INT64] > o.cap_i64 || acc[TFRG_KIND_FLOAT] > o.cap_f32 || acc[TFRG_KIND_BYTES] > o.cap_b)
+      o.info[kInfoOverflow] = 1u;
+    const uint64_t pm = n_slots >= 64u ? ~0ull : (1ull << n_slots) - 1ull;
+    o.info[kInfoPlacedLo] = (uint32_t)pm;
+    o.info[kInfoPlacedHi] = (uint32_t)(pm >> 32);
+  }
+}
+
+// finish: (optimistic decode without shapes) the last workgroup ends the decode, tail_quiet_finish
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kTailBlock, 2) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
-                                                           const uint32_t* __restrict__ consts, uint32_t lane_max) {
+                                                           const uint32_t* __restrict__ consts, uint32_t lane_max,
+                                                           uint32_t finish) {
   role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);
   __syncthreads();  // (the LDS tables are reloaded by role 2)
   role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots);
+  if (finish) {  // (uniform)
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    volatile uint32_t* sh = lds + kTailFinishWord;  // (after role 2's tables)
+    __syncthreads();
+    if (threadIdx.x == 0) sh[0] = atomicAdd(&o.info[kInfoTplDone], 1u) == gridDim.x - 1u;
+    __syncthreads();
+    if (sh[0]) tail_quiet_finish(o, sc.slot_kind, sc.n_slots, B.n, sh[1]);
+  }
 }
 
 // Record queue of a staged wavefront kernel, three stages deep: bytes of the next record (in
@@ -3469,6 +3526,14 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // re-run by the host (tfrg_result_info) if a record took no template. Saves five dependent
   // launches (~4 us each) per batch.
   cfg.ran_optimistic = cfg.optimistic && quiet && all_spec && S > 0;
+  // Optimistic without record shapes (C2: records above lane_max, every slot one inline value in the
+  // learning sample, placed speculatively by k_lane_count MODE 0): k_lane_count, k_tail_count, and
+  // the last workgroup of k_tail_count ends the decode (tail_quiet_finish) or flags it for a full
+  // re-run. Not in strict mode (a CRC failure withdraws a record's columns).
+  const bool quiet_big = cfg.optimistic && !lean && all_spec && S > 0 && lane_lds <= kLaneLdsBudget && fast_ok &&
+                         cfg.body_count && !(b.flags & kFlagStrictCrc) && b.n > 0;
+  cfg.ran_optimistic |= quiet_big;
+  cfg.ran_quiet_big = quiet_big;
   cfg.implicit = 0;
   DevOut ox = o;
   if (!lean) {
@@ -3513,7 +3578,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     const hipError_t e = launch_tpl_lane(b, ox, a, sc.tpl_img, sc.tpl_w, d_tab, cfg.num_cus, st);
     if (e != hipSuccess) return e;
   }
-  if (cfg.ran_optimistic) {  // (k_tpl_lane's last workgroup finished the decode)
+  if (cfg.ran_optimistic && !quiet_big) {  // (k_tpl_lane's last workgroup finished the decode)
     for (int i = kStageLaneCount; i <= kStageMaterialize; ++i) mark(i);
     return hipGetLastError();
   }
@@ -3558,7 +3623,7 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     // (role 1's per-lane dicts for kTailBlock threads, else its global-dict form)
     const size_t slow_tail = 2048ull * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2);
     const bool gord = slow_tail > kLaneLdsBudget;
-    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (19456 + kNumCst) * 4);
+    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (kTailFinishWord + 4) * 4);
     const void* fn = gord ? reinterpret_cast<const void*>(&k_tail_count<COMPAT, true>)
                           : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
     int per_cu = 0;
@@ -3568,12 +3633,17 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     // of batches of small records, is not a full grid of dispatches)
     uint32_t g = std::min((uint32_t)(per_cu * cfg.num_cus), std::max(8u, (uint32_t)(b.nbytes >> 16) + b.n / 4096u));
     if (!cfg.body_count) g = std::min(g, 32u);  // (no record above lane_max: role 2 has nothing to stream)
+    const uint32_t fin = quiet_big ? 1u : 0u;
     if (gord)
       hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab, d_consts,
-                         cfg.lane_max);
+                         cfg.lane_max, fin);
     else
       hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab,
-                         d_consts, cfg.lane_max);
+                         d_consts, cfg.lane_max, fin);
+  }
+  if (quiet_big) {  // (k_tail_count's last workgroup finished the decode)
+    for (int i = kStageSpine; i <= kStageMaterialize; ++i) mark(i);
+    return hipGetLastError();
   }
   if (cfg.poison[0] != 0xffffffffu && S > 0)
     hipLaunchKernelGGL(k_poison_loc, dim3(1), dim3(64), 0, st, ox, b.n, (uint32_t)S,
