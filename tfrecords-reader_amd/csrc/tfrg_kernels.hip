@@ -2020,33 +2020,37 @@ __device__ __forceinline__ CrcEnt crc_ent(const CrcWin& w, uint32_t k) {
   return e;
 }
 
-// the rounds [Rf, Rl] of window entry k, Horner sum S per lane: placed, combined with the other
-// waves' slices of the record, and, once complete, checked against the stored CRC
-__device__ __forceinline__ void crc_flush(const uint8_t* lbase, const uint32_t* __restrict__ ptab, const DevBatch& B,
-                                       const DevOut& o, const CrcWin& w, uint32_t win0,
-                                       uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
-                                       uint32_t n_slots, uint32_t lane) {
-  const uint64_t bas = rl64(w.base, k);
-  const uint32_t J = (uint32_t)(rl64(w.base, k + 1u) - bas);
-  const uint32_t jtop = J - 1u - (uint32_t)(Rf - bas), jlo = J - 1u - (uint32_t)(Rl - bas);
-  uint32_t t = wave_xor_u32(gf_mul(S, cst[lane]));
-  if (jlo) {  // x x^(8192 jlo): one table multiply per set bit of jlo (wave-uniform: scalar loads)
-    uint32_t u = rfl32(t);
-    for (uint32_t kb = 0, jj = jlo; jj; ++kb, jj >>= 1) {
+// Per-record flushes of the streaming CRC, deferred and done 64 at a time, one per lane. A wave
+// flushes a record each time its slice leaves one (C3: ~32 records per wave): the x^(8192 jlo)
+// shift of a split slice, the 64-bit compare-and-swap that combines the slices of a record, the
+// load of its stored CRC and the verdict OR are each a round trip to L2 or HBM, and done at once by
+// the wave they cost ~12 us of C2's 98 us CRC and ~70 us of C3's 390 (flush-less timing builds).
+// Queued here instead (the wave-uniform part, the lane combine of the Horner sums, at once: it needs
+// the lanes' sums), the rest by lane i for the i-th queued record when 64 are pending and at the end
+// of the wave's slice: all the round trips of 64 records in flight together.
+struct CrcFlushQ {
+  uint32_t t, idx, jlo, jtop, J;  // lane i: queued record i (the combined slice value, list entry, rounds)
+  uint32_t n = 0;                 // (wave-uniform) records queued
+};
+
+// lane < q.n: finish queued record `lane` (see crc_flush_push)
+__device__ void crc_flush_run(CrcFlushQ& q, const uint8_t* lbase, const uint32_t* __restrict__ ptab,
+                              const DevBatch& B, const DevOut& o, uint32_t n_slots, uint32_t lane) {
+  if (lane < q.n) {
+    uint32_t t = q.t;
+    const uint32_t idx = q.idx, jlo = q.jlo, jtop = q.jtop, J = q.J;
+    for (uint32_t kb = 0, jj = jlo; jj; ++kb, jj >>= 1) {  // x x^(8192 jlo): one table multiply per set bit
       if (!(jj & 1u)) continue;
       const uint32_t* M = ptab + (size_t)kb * 1024u;
-      u = M[u & 0xffu] ^ M[256u + ((u >> 8) & 0xffu)] ^ M[512u + ((u >> 16) & 0xffu)] ^ M[768u + (u >> 24)];
+      t = M[t & 0xffu] ^ M[256u + ((t >> 8) & 0xffu)] ^ M[512u + ((t >> 16) & 0xffu)] ^ M[768u + (t >> 24)];
     }
-    t = u;
-  }
-  if (jlo != 0u || jtop != J - 1u) {  // a slice of a record split over waves
-    // (rounds done << 32 | XOR of the slices) updated in ONE 64-bit compare-and-swap: the wave that
-    // completes the rounds sees every other slice in the value it replaced, with no fence (an
-    // agent-scope fence per slice wrote back and invalidated L2 under the streaming loads)
-    const uint32_t n_r = jtop - jlo + 1u;
-    uint64_t seen = 0;
-    if (lane == 0) {
-      unsigned long long* p = reinterpret_cast<unsigned long long*>(o.crc_part + (win0 + k));
+    bool complete = true;
+    if (jlo != 0u || jtop != J - 1u) {  // a slice of a record split over waves
+      // (rounds done << 32 | XOR of the slices) updated in ONE 64-bit compare-and-swap: the wave that
+      // completes the rounds sees every other slice in the value it replaced, with no fence (an
+      // agent-scope fence per slice wrote back and invalidated L2 under the streaming loads)
+      const uint32_t n_r = jtop - jlo + 1u;
+      unsigned long long* p = reinterpret_cast<unsigned long long*>(o.crc_part + idx);
       unsigned long long cur = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       for (;;) {
         const unsigned long long nv = ((cur >> 32) + n_r) << 32 | (uint32_t)((uint32_t)cur ^ t);
@@ -2054,35 +2058,55 @@ __device__ __forceinline__ void crc_flush(const uint8_t* lbase, const uint32_t* 
         if (prev == cur) break;
         cur = prev;
       }
-      seen = cur;
+      complete = (uint32_t)(cur >> 32) + n_r == J;  // (else another wave finishes the record)
+      t ^= (uint32_t)cur;
     }
-    seen = rl64(seen, 0);
-    if ((uint32_t)(seen >> 32) + n_r != J) return;  // another wave finishes the record
-    t ^= (uint32_t)seen;
+    if (complete) {
+      const uint32_t r = o.crc_rec[idx];
+      const uint64_t b = rec_view(B, r).e - 4;
+      const uint32_t verdict = o.verdict[r];
+      const uint32_t z = (uint32_t)(16ull * (((b - 1) >> 4) + 1ull) - b);  // zero bytes padding the last chunk
+      // t is the state after the payload and z zero bytes: the stored CRC's state is advanced by the
+      // same z zero bytes through the slicing tables of the rotated layout and compared with t
+      const uint32_t um = load_u32_unaligned(B.bytes, b) - kCrcMaskDelta;
+      uint32_t v = ~((um << 15) | (um >> 17));  // ~crc_mask^-1(stored)
+      auto rt = [&](uint32_t col, uint32_t e) {
+        return *reinterpret_cast<const uint32_t*>(lbase + kRotTabOff + (e << 8) + 4u * col);
+      };
+      uint32_t zz = z;
+      for (; zz >= 4u; zz -= 4u)  // 4 zero bytes: slice-by-4 (tables 3, 2, 1, 0 in columns 2, 1, 0, 15)
+        v = xor3(rt(2u, v & 0xffu), rt(1u, (v >> 8) & 0xffu), rt(0u, (v >> 16) & 0xffu)) ^ rt(15u, v >> 24);
+      for (; zz; --zz) v = (v >> 8) ^ rt(15u, v & 0xffu);
+      if (v == t) {
+        // one atomic OR on the byte's aligned word: a record k_body_count sent back to the exact walker
+        // (role 1 of the same launch) may have its verdict byte written by role 1 at the same time
+        atomicOr(reinterpret_cast<uint32_t*>(o.verdict + (r & ~3u)), (uint32_t)TFRG_V_DATA_CRC << (8u * (r & 3u)));
+      } else if (B.flags & kFlagStrictCrc) {
+        strict_reject(o, B.n, n_slots, r, verdict, 0u, 1u);
+      }
+    }
   }
-  const uint64_t b = rl64(w.b, k);
-  const uint32_t r = rfl32(o.crc_rec[win0 + k]), verdict = o.verdict[r];
-  const uint32_t z = (uint32_t)(16ull * (((b - 1) >> 4) + 1ull) - b);  // zero bytes padding the last chunk
-  // t is the state after the payload and z zero bytes: instead of un-shifting t by x^(-8z) (a 32-step
-  // multiply), the stored CRC's state is advanced by the same z zero bytes through the slicing
-  // tables of the rotated layout (wave-uniform lookups: broadcasts) and compared with t
-  const uint32_t um = load_u32_unaligned(B.bytes, b) - kCrcMaskDelta;
-  uint32_t v = ~((um << 15) | (um >> 17));  // ~crc_mask^-1(stored)
-  auto rt = [&](uint32_t col, uint32_t e) {
-    return *reinterpret_cast<const uint32_t*>(lbase + kRotTabOff + (e << 8) + 4u * col);
-  };
-  uint32_t zz = z;
-  for (; zz >= 4u; zz -= 4u)  // 4 zero bytes: slice-by-4 (tables 3, 2, 1, 0 in columns 2, 1, 0, 15)
-    v = xor3(rt(2u, v & 0xffu), rt(1u, (v >> 8) & 0xffu), rt(0u, (v >> 16) & 0xffu)) ^ rt(15u, v >> 24);
-  for (; zz; --zz) v = (v >> 8) ^ rt(15u, v & 0xffu);
-  if (v == t) {
-    // one atomic OR on the byte's aligned word: a record k_body_count sent back to the exact walker
-    // (role 1 of the same launch) may have its verdict byte written by role 1 at the same time
-    if (lane == 0)
-      atomicOr(reinterpret_cast<uint32_t*>(o.verdict + (r & ~3u)), (uint32_t)TFRG_V_DATA_CRC << (8u * (r & 3u)));
-  } else if (B.flags & kFlagStrictCrc) {
-    strict_reject(o, B.n, n_slots, r, verdict, lane, 64);
+  q.n = 0;
+}
+
+// the rounds [Rf, Rl] of window entry k, Horner sum S per lane: combined over the lanes and queued
+// (crc_flush_run when 64 are pending)
+__device__ __forceinline__ void crc_flush_push(CrcFlushQ& q, const uint8_t* lbase, const uint32_t* __restrict__ ptab,
+                                               const DevBatch& B, const DevOut& o, const CrcWin& w, uint32_t win0,
+                                               uint32_t k, uint64_t Rf, uint64_t Rl, uint32_t S, const uint32_t* cst,
+                                               uint32_t n_slots, uint32_t lane) {
+  const uint64_t bas = rl64(w.base, k);
+  const uint32_t J = (uint32_t)(rl64(w.base, k + 1u) - bas);
+  const uint32_t jtop = J - 1u - (uint32_t)(Rf - bas), jlo = J - 1u - (uint32_t)(Rl - bas);
+  const uint32_t t = wave_xor_u32(gf_mul(S, cst[lane]));
+  if (lane == q.n) {
+    q.t = t;
+    q.idx = win0 + k;
+    q.jlo = jlo;
+    q.jtop = jtop;
+    q.J = J;
   }
+  if (++q.n == 64u) crc_flush_run(q, lbase, ptab, B, o, n_slots, lane);
 }
 
 template <uint32_t BLK>
@@ -2149,6 +2173,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   PHASE_MARK(q1);
   PHASE_ADD(21, q0, q1);
   int cur = -1;  // window entry of the open slice
+  CrcFlushQ fq;  // records whose slices this wave finished, flushed 64 at a time
   uint64_t Rf = 0;
   uint32_t S = 0;
   // Groups of kCrcDepth rounds, double-buffered: the loads of group k+1 are in flight while group k
@@ -2271,7 +2296,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
         S = (tab_at0 ? mul_a1_lds(S) : mul_tab(A1, S)) ^ rc[d];
       }
       if (stop == g.n) break;
-      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush_push(fq, reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, g.r0 + stop - 1, S, cst, n_slots, lane);
       cur = next;
       Rf = g.r0 + stop;
       S = 0;
@@ -2281,7 +2306,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
   uint64_t R = R0;
   while (R < R1) {
     if (R >= lim) {  // next window (R is its first entry's first round)
-      if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
+      if (cur >= 0) crc_flush_push(fq, reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R - 1, S, cst, n_slots, lane);
       cur = -1;
       win0 += 63u;
       w = crc_win_load(B, o, win0, nrec, TR, lane);
@@ -2303,7 +2328,8 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
       if (!ga.n) break;
     }
   }
-  if (cur >= 0) crc_flush(reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
+  if (cur >= 0) crc_flush_push(fq, reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, w, win0, (uint32_t)cur, Rf, R1 - 1, S, cst, n_slots, lane);
+  if (fq.n) crc_flush_run(fq, reinterpret_cast<const uint8_t*>(lds), crc_tab + kPowTabOff, B, o, n_slots, lane);
   PHASE_MARK(q9);
   PHASE_ADD(25, q0, q9);
 }

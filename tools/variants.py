@@ -112,6 +112,11 @@ VARIANTS = {
     # k_tpl_lane at 7 waves/SIMD (72 VGPRs)
     "lb7": [("tfrg_tpl.hip", "__launch_bounds__(kTplBlock, W == 16 ? 6 : (W == 32 ? 4 : 2))",
              "__launch_bounds__(kTplBlock, W == 16 ? 7 : (W == 32 ? 4 : 2))")],
+    # the streaming CRC's per-record flush (timing only, wrong verdicts): none of it / without the
+    # x^(8192 jlo) shift of split slices
+    "flush_none": [("tfrg_kernels.hip", "                                       uint32_t n_slots, uint32_t lane) {\n  const uint64_t bas = rl64(w.base, k);",
+                    "                                       uint32_t n_slots, uint32_t lane) {\n  if (n_slots != 0xfffffffeu) return;\n  const uint64_t bas = rl64(w.base, k);")],
+    "flush_nojlo": [("tfrg_kernels.hip", "  if (jlo) {  // x x^(8192 jlo)", "  if (jlo && n_slots == 0xfffffffeu) {  // x x^(8192 jlo)")],
 }
 
 
