@@ -136,7 +136,9 @@ int tfrg_ctx_set_wave_stage(tfrg_ctx* ctx, uint32_t nbytes);
  * gets the template's dict without a walk (its values are still read from the record; k_tpl_lane,
  * schemas of <= TFRG_TPL_MAX_SLOTS slots, CRC verdicts on); any other record takes the canonical walk.
  * Learned automatically from the first tfrg_decode_host batch after each tfrg_set_schema; device-only
- * callers pass a host sample here. Returns the number of templates (0..TFRG_TPL_MAX).
+ * callers pass a host sample here. Returns the number of templates (0..TFRG_TPL_MAX). With no shape
+ * kept, the slots that are one inline value in every sampled record (host decode) are still learned
+ * for speculative placement (the optimistic decode of large single-value records).
  * tfrg_ctx_set_templates(ctx, 0) disables the match (env TFRG_TEMPLATES=0); the speculative
  * placement of slots that are one inline value in every learned shape stays on. */
 #define TFRG_TPL_MAX 32
