@@ -117,6 +117,15 @@ VARIANTS = {
     "flush_none": [("tfrg_kernels.hip", "                                       uint32_t n_slots, uint32_t lane) {\n  const uint64_t bas = rl64(w.base, k);",
                     "                                       uint32_t n_slots, uint32_t lane) {\n  if (n_slots != 0xfffffffeu) return;\n  const uint64_t bas = rl64(w.base, k);")],
     "flush_nojlo": [("tfrg_kernels.hip", "  if (jlo) {  // x x^(8192 jlo)", "  if (jlo && n_slots == 0xfffffffeu) {  // x x^(8192 jlo)")],
+    # k_tail_count: the streaming CRC (role 2) before the exact walker (role 1), so its prologue does
+    # not wait for role 1's slow-list count
+    "role2first": [("tfrg_kernels.hip", """  role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);
+  __syncthreads();  // (the LDS tables are reloaded by role 2)
+  role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots);
+  if (finish) {""", """  role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots);
+  __syncthreads();  // (the LDS tables are reloaded by role 1)
+  role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);
+  if (finish) {""")],
 }
 
 
