@@ -85,6 +85,39 @@ def test_optimistic_large_records_identical_and_rerun_on_a_miss(monkeypatch):
         full.close()
 
 
+@pytest.mark.parametrize("walk", [("1", "1"), ("0", "0")], ids=["beside_one_workgroup", "before_crc"])
+def test_optimistic_large_records_walk_modes(monkeypatch, walk):
+    """The large records walked beside the streaming CRC by ONE workgroup of k_tail_count (each of its
+    waves then walks several 64-record groups, role_big_walk), and walked before it by k_lane_count
+    (TFRG_WALK_BESIDE=0): both identical to the decode with every pass, a miss re-run in full."""
+    monkeypatch.setenv("TFRG_WALK_BESIDE", walk[0])
+    monkeypatch.setenv("TFRG_WALK_BLOCKS", walk[1])
+    on, full = _pair(monkeypatch)
+    try:
+        buf, st, en = synth.framed(_flowers(600, 12))
+        on.decode(buf, st, en)
+        full.decode(buf, st, en)
+        buf, st, en = synth.framed(_flowers(1500, 13))  # (24 groups: 3 per wave of the one workgroup)
+        bad = buf.copy()
+        bad[int(st[700]) + 12 + 3000] ^= 0x01  # (an image byte: record 700's payload CRC fails, verdict 3)
+        a, b = on.decode(bad, st, en), full.decode(bad, st, en)
+        assert on.device_bytes()[1] == 0  # (a CRC verdict is no miss: no re-run)
+        _same(a, b)
+        assert (a.status == 0).all() and int(a.verdict[700]) == 3
+        assert (np.delete(np.array(a.verdict), 700) == 7).all()
+        _check_oracle(a, bad, st, en, [700] + list(range(3, 1500, 53)))
+        odd = {1400: [("image", "bytes_list", [b"q" * 9000]), ("label", "int64_list", [1, 2, 3]),
+                      ("file_name", "bytes_list", [b"three_labels.jpg"])]}
+        buf, st, en = synth.framed(_flowers(1500, 14, odd))
+        a, b = on.decode(buf, st, en), full.decode(buf, st, en)
+        assert on.device_bytes()[1] == 1
+        _same(a, b)
+        _check_oracle(a, buf, st, en, [1400] + list(range(0, 1500, 61)))
+    finally:
+        on.close()
+        full.close()
+
+
 def test_optimistic_large_records_device_view_and_strict(monkeypatch):
     """The device view straight after a device decode confirms it; strict CRC mode takes every pass."""
     import torch

@@ -152,6 +152,8 @@ struct tfrg_ctx {
   // sample is launched as k_tpl_lane alone (its last workgroup finishes it); the decode is complete once tfrg_result_info
   // (or tfrg_result_device) has read that no record was left, else it is re-run with every pass
   bool optimistic_on = true;  // (env TFRG_OPTIMISTIC=0: off, for A/B measurements)
+  bool walk_beside = true;    // (env TFRG_WALK_BESIDE=0: large records walked before the CRC, A/B)
+  uint32_t walk_blocks = 0;   // (env TFRG_WALK_BLOCKS: cap on its walking workgroups; 0 = automatic)
   bool no_quiet = false;      // (the re-run)
   bool opt_pending = false;   // the last decode ran optimistically and is not confirmed yet
   bool ord_const = false;     // (Learned::ord_const) of the learned shapes
@@ -189,6 +191,8 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
   if (const char* e = getenv("TFRG_TEMPLATES")) c->tpl_on = atoi(e) != 0;  // (A/B measurements)
   if (const char* e = getenv("TFRG_SPEC")) c->spec_on = atoi(e) != 0;
   if (const char* e = getenv("TFRG_OPTIMISTIC")) c->optimistic_on = atoi(e) != 0;
+  if (const char* e = getenv("TFRG_WALK_BESIDE")) c->walk_beside = atoi(e) != 0;
+  if (const char* e = getenv("TFRG_WALK_BLOCKS")) c->walk_blocks = (uint32_t)atoi(e);
   if (const char* e = getenv("TFRG_DEBUG_POISON_LOC")) {  // "r0,r1,..." (at most 4)
     char* q = const_cast<char*>(e);
     for (int i = 0; i < 4 && *q; ++i) {
@@ -1153,6 +1157,8 @@ static int decode_device_any(tfrg_ctx* c, const uint8_t* d_bytes, uint64_t nbyte
   memcpy(cfg.poison, c->poison, sizeof(cfg.poison));
   // (the poison hook needs the gathers it tests)
   cfg.optimistic = c->optimistic_on && !c->no_quiet && c->poison[0] == 0xffffffffu;
+  cfg.walk_beside = c->walk_beside;
+  cfg.walk_blocks = c->walk_blocks;
   cfg.ran_optimistic = false;
   cfg.ran_quiet_big = false;
   cfg.ord_const = c->ord_const;

@@ -199,6 +199,8 @@ enum InfoIdx : uint32_t {
                          // they listed << 32 (one atomic: the last workgroup knows the total)
   kInfoBigRecs = 22,     // records above lane_max (tfrg_info.n_big; kInfoBig + kInfoHuge count the
                          // ones listed for the wave gathers: those with out-of-line lists)
+  kInfoWalkMiss = 23,    // records above lane_max walked beside the CRC (k_tail_count) that the
+                         // canonical walker did not take or that have an out-of-line list: re-run
   kInfoCount = 24        // (even: the two slots' u64 words stay 8-byte aligned)
 };
 static_assert(kInfoCount % 2 == 0 && kInfoCrcCtr % 2 == 0 && kInfoTplDone % 2 == 0,
@@ -319,6 +321,9 @@ struct LaunchCfg {
   bool ord_const;          // every learned shape has every slot at the same key position
   bool len_const;          // every bytes slot one element of one length in every learned shape
   bool ran_quiet_big;      // (out) optimistic without shapes: k_tail_count's last workgroup ends it
+  bool walk_beside;        // optimistic without shapes: records above lane_max walked beside the CRC
+                           // (k_tail_count's first workgroups) instead of before it (k_lane_count)
+  uint32_t walk_blocks;    // cap on those workgroups (0: automatic)
   uint32_t implicit;       // (out) TFRG_IMPLICIT_* columns the decode did not store
 };
 

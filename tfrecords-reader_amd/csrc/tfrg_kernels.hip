@@ -1361,7 +1361,8 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t x) {
 template <int R, bool COMPAT, int MODE>
 __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_count(DevBatch B, DevSchema sc, DevOut o,
                                                                                   const uint32_t* __restrict__ crc_tab,
-                                                                                  uint32_t lane_max, uint32_t wave_stage) {
+                                                                                  uint32_t lane_max, uint32_t wave_stage,
+                                                                                  uint32_t defer_big) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   // slicing tables at a static LDS address: lookups fold the table base into the ds_read offset
   __shared__ uint32_t tab[256 * kLaneSlice * R];
@@ -1449,6 +1450,9 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
       big = v.status == TFRG_OK && v.e - v.st > lane_max;  // (listed for the wave gathers below)
       mine = !big;
     }
+    // (defer_big: a record above lane_max is walked by k_tail_count beside the streaming CRC,
+    // role_big_walk; here it is only listed for the CRC and its verdict byte cleared)
+    const bool deferred = defer_big && big;
     {
       const uint64_t bm = __ballot(big);
       if (bm && lane == 0) atomicAdd(&o.info[kInfoBigRecs], (uint32_t)__popcll(bm));
@@ -1502,7 +1506,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     // canonical walk straight from HBM, one record per lane (64 latency chains in flight per wave).
     // The payload CRC of records above lane_max is the streaming CRC's (k_tail_count role 2); the
     // others' is computed here, serially per lane from HBM.
-    const bool bigw = fast_ok && valid && (!mine || (span_rec && !staged));
+    const bool bigw = fast_ok && valid && !deferred && (!mine || (span_rec && !staged));
     if (__ballot(bigw)) {
       // one block of deferred-body rows per wave (k_body_count), while the batch has room
       uint32_t blk = ~0u;
@@ -1532,7 +1536,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     }
     PHASE_MARK(p4);
     // everything else of this wave's records goes to the exact walker
-    const bool slow = valid && !done;
+    const bool slow = valid && !done && !deferred;
     const uint64_t sm = __ballot(slow);
     if (sm) {
       uint32_t b0 = 0;
@@ -1546,11 +1550,13 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     if (done) {
       o.status[r] = TFRG_OK;
       o.verdict[r] = (uint8_t)v.verdict;
+    } else if (deferred) {
+      o.verdict[r] = 0;  // (bits OR-ed in by role_big_walk and role 2)
     }
-    // the payload CRC of an accepted large record: one entry of the streaming CRC list
+    // the payload CRC of an accepted (or deferred) large record: one entry of the streaming CRC list
     const bool crc_on = !(B.flags & (kFlagPayloadOnly | kFlagNoCrc));
     const uint32_t crc_j =
-        done && !mine && crc_on && v.e - v.st >= 16 && (uint64_t)v.L >= kCrcListMin ? crc_rounds_of(v.p0, v.e - 4) : 0u;
+        (done || deferred) && !mine && crc_on && v.e - v.st >= 16 && (uint64_t)v.L >= kCrcListMin ? crc_rounds_of(v.p0, v.e - 4) : 0u;
     // order / count columns of the accepted records + the tile sums (one atomic per slot and wave)
     if constexpr (MODE == 1) {
       if (tried && !done) sink.rollback();
@@ -1585,7 +1591,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
           // (the row splits of a final placement are implicit for the first 64 slots:
           // tfrg_info.placed_slots; a failed placement has them all rewritten by k_down_gather)
           if (valid && k >= 64u) o.rs[(size_t)k * (B.n + 1) + r] = r;
-          const uint64_t irm = __ballot(valid && !(done && c == (1u | kCountInline)));
+          const uint64_t irm = __ballot(valid && !deferred && !(done && c == (1u | kCountInline)));
           if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
         }
       }
@@ -1594,7 +1600,7 @@ __global__ __launch_bounds__(kLaneCountBlock, MODE == 0 ? 6 : 4) void k_lane_cou
     // a large record goes to the wave gathers (staged ones from the front of big_list, huge ones
     // from the back) if it has a list k_down_gather does not write: out-of-line or deferred lists, or
     // any list of a record the exact walker takes (C2's single image views and labels need none)
-    if (big && (!done || ool || nd)) {
+    if (big && !deferred && (!done || ool || nd)) {
       if (v.e - (v.st & ~15ull) <= wave_stage) {
         const uint32_t i = atomicAdd(&o.info[kInfoBig], 1u);
         o.big_list[i] = r;
@@ -1684,7 +1690,7 @@ __global__ __launch_bounds__(kBodyBlock) void k_body_count(DevBatch B, DevOut o)
 // Exact reference walk (decoder.pyx:107-300 in its own level-by-level error precedence), one lane per
 // record of the slow list, reading the record from HBM; also the framing errors and schema misses.
 template <int R, bool COMPAT, bool GORD, uint32_t BLK>
-__device__ void role_slow_count(const DevBatch& B, const DevSchema& sc, const DevOut& o,
+__device__ __forceinline__ void role_slow_count(const DevBatch& B, const DevSchema& sc, const DevOut& o,
                                 const uint32_t* __restrict__ crc_tab, uint32_t lane_max) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   const uint32_t nslow = o.info[kInfoSlow];
@@ -2109,9 +2115,10 @@ __device__ __forceinline__ void crc_flush_push(CrcFlushQ& q, const uint8_t* lbas
   if (++q.n == 64u) crc_flush_run(q, lbase, ptab, B, o, n_slots, lane);
 }
 
+// (wb: the launch's first wb workgroups walk large records instead, role_big_walk)
 template <uint32_t BLK>
 __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut& o, const uint32_t* __restrict__ crc_tab,
-                                const uint32_t* __restrict__ consts, uint32_t n_slots) {
+                                const uint32_t* __restrict__ consts, uint32_t n_slots, uint32_t wb) {
   extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
   if (B.flags & (kFlagPayloadOnly | kFlagNoCrc)) return;
   const uint64_t ctr = *reinterpret_cast<const uint64_t*>(o.info + kInfoCrcCtr);
@@ -2145,7 +2152,7 @@ __device__ __forceinline__ void role_crc_stream(const DevBatch& B, const DevOut&
       0x00020000);
   const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
   const CrcRot RR = crc_rot_init(lane);
-  const uint64_t W = (uint64_t)gridDim.x * (BLK / 64), wv = (uint64_t)blockIdx.x * (BLK / 64) + wib;
+  const uint64_t W = (uint64_t)(gridDim.x - wb) * (BLK / 64), wv = (uint64_t)(blockIdx.x - wb) * (BLK / 64) + wib;
   const uint64_t R0 = TR * wv / W, R1 = TR * (wv + 1) / W;
   const bool work = R0 < R1;  // (wave-uniform)
   PHASE_MARK(q0);
@@ -2357,11 +2364,12 @@ constexpr uint32_t kTailFinishWord = 19456 + kNumCst;  // two LDS words of the f
 // host before the next decode.)
 // (s_ok: a word of the dynamic LDS; a static __shared__ object would move the dynamic region off LDS
 // address 0, which role 2's table lookups address directly)
-__device__ void tail_quiet_finish(const DevOut& o, const uint8_t* slot_kind, uint32_t n_slots, uint32_t n,
+__device__ __forceinline__ void tail_quiet_finish(const DevOut& o, const uint8_t* slot_kind, uint32_t n_slots, uint32_t n,
                                   volatile uint32_t& s_ok) {
   if (threadIdx.x == 0) {
     s_ok = o.info[kInfoSlow] == 0u && o.info[kInfoMissRecords] == 0u && o.info[kInfoErrors] == 0u &&
-           o.info[kInfoBig] == 0u && o.info[kInfoHuge] == 0u && o.info[kInfoDefer] == 0u;
+           o.info[kInfoBig] == 0u && o.info[kInfoHuge] == 0u && o.info[kInfoDefer] == 0u &&
+           o.info[kInfoWalkMiss] == 0u;
   }
   __syncthreads();
   if (threadIdx.x < n_slots && o.irr[threadIdx.x] != 0u) s_ok = 0u;  // (benign race: only zeroes)
@@ -2392,15 +2400,109 @@ __device__ void tail_quiet_finish(const DevOut& o, const uint8_t* slot_kind, uin
   }
 }
 
-// finish: (optimistic decode without shapes) the last workgroup ends the decode, tail_quiet_finish
+// Optimistic decodes without record shapes (k_tail_count's first `walk_blocks` workgroups): the
+// records above lane_max, walked while the other workgroups stream their payload CRC (role 2) instead
+// of by k_lane_count before it. C2's records are all above lane_max: walking them one per lane is a
+// chain of dependent HBM round trips per map entry (~27 us on 128 waves) that left the CRC waiting.
+// k_lane_count (defer_big) listed them for the CRC and cleared their verdict bytes; the framing bits
+// are OR-ed in here, the payload CRC's by role 2, into the same words. The columns, tile sums and
+// irregular counts are those k_lane_count MODE 0 writes for a record it walks from HBM (with the
+// 32-byte register window: this launch's register budget has room for it). A record the canonical
+// walker does not take, or one with an out-of-line list, flags the batch for a full re-run
+// (kInfoWalkMiss, read by tail_quiet_finish).
+template <bool COMPAT>
+__device__ __forceinline__ void role_big_walk(const DevBatch& B, const DevSchema& sc, const DevOut& o, const uint32_t* __restrict__ crc_tab,
+                              uint32_t lane_max, uint32_t walk_blocks) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+  constexpr uint32_t BLK = kTailBlock, kW = BLK / 64;
+  const uint32_t S = sc.n_slots;
+  // layout (launch_all: walk_lds): slicing tables, per-lane dict (counts, ranks), keys, spec targets
+  uint32_t* tab = lds;
+  uint32_t* cnt = tab + 256u * kLaneSlice;
+  uint16_t* ord = reinterpret_cast<uint16_t*>(cnt + S * BLK);
+  uint32_t* kht = cnt + S * BLK + ((S * BLK * 2u + 15u) & ~15u) / 4u;
+  uint32_t* krec = kht + ((sc.ht_mask + 4u) & ~3u);
+  uint32_t* spec_l = krec + sc.n_keys * kKrWords;
+  uint32_t* spec_tl = spec_l + ((S + 7u) & ~7u);  // (16-byte aligned)
+  for (uint32_t i = threadIdx.x; i < 256u * kLaneSlice; i += BLK) tab[i] = crc_tab[2048 + i];
+  for (uint32_t i = threadIdx.x; i <= sc.ht_mask; i += BLK) kht[i] = sc.ht[i];
+  for (uint32_t i = threadIdx.x; i < sc.n_keys * kKrWords; i += BLK) krec[i] = sc.krec[i];
+  for (uint32_t i = threadIdx.x; i < S; i += BLK) {
+    spec_l[i] = sc.spec[i];
+    spec_target(spec_tl + kSpecTgtWords * i, o, sc.spec[i], B.n);
+  }
+  __syncthreads();
+  const LdsKeys K{kht, krec, sc.ht_mask, sc.key_blob, sc.key_off};
+  const LdsTab<1> T{tab, 0u};
+  const uint32_t lane = threadIdx.x & 63u, wib = rfl32(threadIdx.x >> 6);
+  const uint32_t ng = (B.n + 63u) >> 6, nw = walk_blocks * kW;
+  uint32_t miss = 0;
+  for (uint32_t g = blockIdx.x * kW + wib; g < ng; g += nw) {  // (wave-uniform)
+    const uint32_t r = g * 64u + lane;
+    const uint32_t tile = (g * 64u) >> kTileShift;
+    RecView v{};
+    bool big = false;
+    if (r < B.n) {
+      v = rec_view(B, r);
+      big = v.status == TFRG_OK && v.e - v.st > lane_max;
+    }
+    if (!__ballot(big)) continue;
+    CountSinkT<true> sink{&sc, &o, (lds_u16*)(ord + threadIdx.x), BLK, 0, B.n, r, v.p0, false, true};
+    sink.cnt = (lds_u32*)(cnt + threadIdx.x);
+    sink.spec = (const lds_u32*)spec_l;
+    sink.spec_t = (const lds_spec_t*)spec_tl;
+    bool done = false;
+    if (big) {
+      // (the payload CRC is role 2's unless the payload is shorter than one round: k_lane_count's rule)
+      frame_verdicts<1, false>(B, v, T, nullptr, 0, (uint64_t)v.L < kCrcListMin);
+      sink.fast_reset(S);
+      const FastSrcG<true> fg{B.bytes, v.p0, (uint32_t)v.L, ((B.nbytes + 15) & ~15ull) - 4};
+      done = fast_walk<COMPAT>(fg, K, sink) == TFRG_OK;
+    }
+    bool ool = false;
+    for (uint32_t k = 0; k < S; ++k) {
+      const uint32_t ov = done ? (uint32_t)sink.ord[(size_t)k * BLK] : 0u;
+      const uint32_t c = ov ? sink.count_of(k) : 0u;
+      ool |= c != 0u && !(c & kCountInline);
+      if (done) {
+        const size_t at = (size_t)k * B.n + r;
+        o.order[at] = (uint16_t)ov;
+        o.count[at] = c;
+      }
+      const uint32_t x = c & ~kCountInline;
+      const uint64_t nz = __ballot(x != 0u);
+      if (nz) {
+        const uint32_t t = __ballot(x > 1u) ? wave_sum_u32(x) : (uint32_t)__popcll(nz);
+        if (lane == 0) atomicAdd(&o.tsum[(size_t)k * o.tile_stride + tile], t);
+      }
+      if (spec_l[k]) {  // (wave-uniform)
+        const uint64_t irm = __ballot(big && !(done && c == (1u | kCountInline)));
+        if (irm && lane == 0) atomicAdd(&o.irr[k], (uint32_t)__popcll(irm));
+      }
+    }
+    if (done) {
+      o.status[r] = TFRG_OK;
+      atomicOr(reinterpret_cast<uint32_t*>(o.verdict + (r & ~3u)), (uint32_t)v.verdict << (8u * (r & 3u)));
+    }
+    miss += (uint32_t)__popcll(__ballot(big && (!done || ool)));
+  }
+  if (miss && lane == 0) atomicAdd(&o.info[kInfoWalkMiss], miss);
+}
+
+// finish: (optimistic decode without shapes) the last workgroup ends the decode, tail_quiet_finish;
+// walk_blocks: its first workgroups walk the records above lane_max (role_big_walk), the others
+// stream the CRC
 template <bool COMPAT, bool GORD>
 __global__ __launch_bounds__(kTailBlock, 2) void k_tail_count(DevBatch B, DevSchema sc, DevOut o,
                                                            const uint32_t* __restrict__ crc_tab,
                                                            const uint32_t* __restrict__ consts, uint32_t lane_max,
-                                                           uint32_t finish) {
+                                                           uint32_t finish, uint32_t walk_blocks) {
   role_slow_count<1, COMPAT, GORD, kTailBlock>(B, sc, o, crc_tab, lane_max);
   __syncthreads();  // (the LDS tables are reloaded by role 2)
-  role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots);
+  if (blockIdx.x < walk_blocks)  // (block-uniform)
+    role_big_walk<COMPAT>(B, sc, o, crc_tab, lane_max, walk_blocks);
+  else
+    role_crc_stream<kTailBlock>(B, o, crc_tab, consts, sc.n_slots, walk_blocks);
   if (finish) {  // (uniform)
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     volatile uint32_t* sh = lds + kTailFinishWord;  // (after role 2's tables)
@@ -3560,6 +3662,15 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
                          cfg.body_count && !(b.flags & kFlagStrictCrc) && b.n > 0;
   cfg.ran_optimistic |= quiet_big;
   cfg.ran_quiet_big = quiet_big;
+  // k_tail_count's LDS (role 1's per-lane dicts for kTailBlock threads, else its global-dict form;
+  // role 2's tables and the finishing words)
+  const size_t slow_tail = 2048ull * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2);
+  const bool tail_gord = slow_tail > kLaneLdsBudget;
+  const size_t tail_lds = std::max<size_t>(tail_gord ? 2048ull * 4 : slow_tail, (kTailFinishWord + 4) * 4);
+  // quiet_big: the records above lane_max walked beside the streaming CRC by k_tail_count's first
+  // workgroups (role_big_walk) when its per-lane dicts fit the launch's LDS
+  const size_t walk_lds = 256ull * kLaneSlice * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2) + keys_lds + spec_lds;
+  const bool walk_beside = quiet_big && cfg.walk_beside && walk_lds <= tail_lds;
   cfg.implicit = 0;
   DevOut ox = o;
   if (!lean) {
@@ -3625,17 +3736,18 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   if (lane_lds <= kLaneLdsBudget) {
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 0>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 0>), dim3(resident_grid(fn, lane_lds - tab_lds)),
-                       dim3(kLaneCountBlock), lane_lds - tab_lds, st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
+                       dim3(kLaneCountBlock), lane_lds - tab_lds, st, b, scx, ox, d_tab, cfg.lane_max, wave_stage,
+                       walk_beside ? 1u : 0u);
   } else if (S <= 64) {
     const size_t lds = stage_lds + keys_lds + (kLaneCountBlock / 64) * 64 * 4;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 1>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 1>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
-                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage, 0u);
   } else {
     const size_t lds = stage_lds + keys_lds;  // (+ the static tables)
     const void* fn = reinterpret_cast<const void*>(&k_lane_count<kLaneRep, COMPAT, 2>);
     hipLaunchKernelGGL((k_lane_count<kLaneRep, COMPAT, 2>), dim3(resident_grid(fn, lds)), dim3(kLaneCountBlock), lds,
-                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage);
+                       st, b, scx, ox, d_tab, cfg.lane_max, wave_stage, 0u);
   }
   mark(kStageBodyCount);
   if (cfg.body_count && lane_lds > kLaneLdsBudget) {  // deferred bodies (lane modes 1 and 2 only)
@@ -3646,10 +3758,8 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
   // the exception paths before the scan: one launch, one round of resident workgroups (role 2 splits
   // the large payloads evenly over the waves; role 1 grid-strides over the slow list)
   {
-    // (role 1's per-lane dicts for kTailBlock threads, else its global-dict form)
-    const size_t slow_tail = 2048ull * 4 + S * kTailBlock * 4 + r16(S * kTailBlock * 2);
-    const bool gord = slow_tail > kLaneLdsBudget;
-    const size_t lds = std::max<size_t>(gord ? 2048ull * 4 : slow_tail, (kTailFinishWord + 4) * 4);
+    const bool gord = tail_gord;
+    const size_t lds = tail_lds;
     const void* fn = gord ? reinterpret_cast<const void*>(&k_tail_count<COMPAT, true>)
                           : reinterpret_cast<const void*>(&k_tail_count<COMPAT, false>);
     int per_cu = 0;
@@ -3660,12 +3770,23 @@ static hipError_t launch_all(const DevBatch& b, const DevSchema& sc, const DevOu
     uint32_t g = std::min((uint32_t)(per_cu * cfg.num_cus), std::max(8u, (uint32_t)(b.nbytes >> 16) + b.n / 4096u));
     if (!cfg.body_count) g = std::min(g, 32u);  // (no record above lane_max: role 2 has nothing to stream)
     const uint32_t fin = quiet_big ? 1u : 0u;
+    // the walking workgroups: one 64-record group per wave, at most 1/32 of the grid (the streaming
+    // CRC is bound by its workgroups' issue rate: each one it loses costs it 1/g of its time, while a
+    // walking wave takes several groups well within the CRC's time). Every workgroup of the grid is
+    // resident, the walkers dispatched first.
+    uint32_t wb = 0;
+    if (walk_beside) {
+      if (g < 2u) g = 2u;
+      const uint32_t ng = (uint32_t)((b.n + 63) / 64);
+      const uint32_t cap = cfg.walk_blocks ? cfg.walk_blocks : std::max(1u, g / 32u);
+      wb = std::max(1u, std::min({(ng + kTailBlock / 64 - 1) / (kTailBlock / 64), cap, g - 1u}));
+    }
     if (gord)
       hipLaunchKernelGGL((k_tail_count<COMPAT, true>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab, d_consts,
-                         cfg.lane_max, fin);
+                         cfg.lane_max, fin, wb);
     else
       hipLaunchKernelGGL((k_tail_count<COMPAT, false>), dim3(g), dim3(kTailBlock), lds, st, b, scx, ox, d_tab,
-                         d_consts, cfg.lane_max, fin);
+                         d_consts, cfg.lane_max, fin, wb);
   }
   if (quiet_big) {  // (k_tail_count's last workgroup finished the decode)
     for (int i = kStageSpine; i <= kStageMaterialize; ++i) mark(i);
