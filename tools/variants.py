@@ -129,6 +129,10 @@ VARIANTS = {
 }
 
 
+VARIANTS["noboff"] = [("tfrg_tpl.hip", "                reinterpret_cast<uint32_t*>(T.v1)[r] = lx;\n                if (T.kind == TFRG_KIND_BYTES",
+                        "                if (T.kind != TFRG_KIND_BYTES) reinterpret_cast<uint32_t*>(T.v1)[r] = lx;\n                if (T.kind == TFRG_KIND_BYTES")]  # (measurement only: the bytes offsets not stored)
+
+
 def build(name: str) -> Path:
     with tempfile.TemporaryDirectory() as td:
         d = Path(td) / "pkg" / "csrc"  # (the sources include ../../include)
