@@ -133,6 +133,18 @@ VARIANTS["noboff"] = [("tfrg_tpl.hip", "                reinterpret_cast<uint32_
                         "                if (T.kind != TFRG_KIND_BYTES) reinterpret_cast<uint32_t*>(T.v1)[r] = lx;\n                if (T.kind == TFRG_KIND_BYTES")]  # (measurement only: the bytes offsets not stored)
 
 
+# (measurement only) the streaming CRC's loads and group structure without its arithmetic: what the
+# role-2 load pattern achieves on its own (wrong verdicts)
+VARIANTS["crc_loadonly"] = [("tfrg_kernels.hip", """  auto process = [&](const Grp& g) {
+""", """  auto process = [&](const Grp& g) {
+    if (n_slots != 0xfffffffeu) {
+#pragma unroll
+      for (int d = 0; d < kCrcDepth; ++d) S ^= g.wd[d].x ^ g.wd[d].y ^ g.wd[d].z ^ g.wd[d].w;
+      return;
+    }
+""")]
+
+
 def build(name: str) -> Path:
     with tempfile.TemporaryDirectory() as td:
         d = Path(td) / "pkg" / "csrc"  # (the sources include ../../include)
