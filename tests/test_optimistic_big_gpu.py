@@ -113,6 +113,17 @@ def test_optimistic_large_records_walk_modes(monkeypatch, walk):
         assert on.device_bytes()[1] == 1
         _same(a, b)
         _check_oracle(a, buf, st, en, [1400] + list(range(0, 1500, 61)))
+        # a record whose payload is not an Example (a truncated map entry): the exact walker's error,
+        # re-run in full; its neighbours decode
+        buf, st, en = synth.framed(_flowers(1500, 15))
+        bad = buf.copy()
+        bad[int(st[900]) + 12 + 1] ^= 0x7f  # (the Features length varint of record 900)
+        runs = on.device_bytes()[1]
+        a, b = on.decode(bad, st, en), full.decode(bad, st, en)
+        assert on.device_bytes()[1] == runs + 1
+        _same(a, b)
+        assert int(a.status[900]) != 0 and int(a.info.n_errors) == 1
+        assert (np.delete(np.array(a.status), 900) == 0).all()
     finally:
         on.close()
         full.close()
