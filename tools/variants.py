@@ -145,6 +145,23 @@ VARIANTS["crc_loadonly"] = [("tfrg_kernels.hip", """  auto process = [&](const G
 """)]
 
 
+# (measurement) streaming-CRC groups that never cross a record (a record's last group is partial;
+# its unused loads repeat the group's last chunk instead of reading ahead)
+VARIANTS["crc_align"] = [("tfrg_kernels.hip", """    if (!g.n) return;
+    const uint64_t rl = Rs + g.n - 1u;
+    const uint32_t k0 = (uint32_t)__popcll(__ballot(w.base <= Rs)) - 1u;
+    const uint32_t kl = (uint32_t)__popcll(__ballot(w.base <= rl)) - 1u;""", """    if (!g.n) return;
+    const uint32_t k0 = (uint32_t)__popcll(__ballot(w.base <= Rs)) - 1u;
+    {
+      const uint64_t re = rl64(w.base, k0 + 1u);
+      if (Rs + g.n > re) g.n = (uint32_t)(re - Rs);
+    }
+    const uint64_t rl = Rs + g.n - 1u;
+    const uint32_t kl = k0;"""),
+    ("tfrg_kernels.hip", """        g.wd[d] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo + 1024u * d, 0, 0));""",
+     """        g.wd[d] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(brs, vo + 1024u * ((uint32_t)d < g.n ? (uint32_t)d : g.n - 1u), 0, 0));""")]
+
+
 def build(name: str) -> Path:
     with tempfile.TemporaryDirectory() as td:
         d = Path(td) / "pkg" / "csrc"  # (the sources include ../../include)
