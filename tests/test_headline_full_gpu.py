@@ -7,6 +7,8 @@ deterministic generator wrote, record by record, vectorised:
   ~16.8 M records, ~0.99 GB) in the library's default 1 GiB batches;
 * bench.py's N = 1 batch plan: the first files of the directory, > 2 GiB, in the bench's 2 GiB
   batches (one full 2 GiB batch of ~36 M records, batch offsets up to 2^31 - 2, plus the rest);
+* the largest batch a decode call takes: one batch just under 4 GiB (~73 M records, byte offsets
+  and views above 2^31), plus the rest;
 
 * status OK and verdict 7 (length field, length CRC and payload CRC all match) for every record;
 * the dict order of every record: ``label`` first, ``id`` second (reader order, decoder.pyx:107-199);
@@ -119,3 +121,12 @@ def test_headline_2gib_batch_plan_values():
     sizes = synth.c4_file_sizes(N_FILES, "c1")
     k = int(np.searchsorted(np.cumsum(sizes), (1 << 31) + (1 << 28))) + 1  # > 2.25 GiB of files
     _check(list(range(k)), 1 << 31)
+
+
+def test_headline_max_batch_values():
+    """The largest batch a decode call takes (< 4 GiB, u32 byte views and offsets above 2^31): one
+    batch just under 4 GiB of C1-shaped files (~73 M records) plus the rest, on two streams."""
+    sizes = synth.c4_file_sizes(N_FILES, "c1")
+    cap = (1 << 32) - (1 << 24)
+    k = int(np.searchsorted(np.cumsum(sizes), cap + (1 << 26))) + 1
+    _check(list(range(k)), cap)
