@@ -160,6 +160,7 @@ struct tfrg_ctx {
   bool len_const = false;     // (Learned::len_const)
   std::vector<uint32_t> const_len;  // per slot: the bytes element length of every learned shape
   uint32_t last_implicit = 0; // TFRG_IMPLICIT_* columns the last decode did not store
+  uint32_t* info_pin = nullptr;  // pinned host copy of the info words + kind totals (confirmation)
   bool cols_complete = false; // tfrg_result_device filled them into the device columns
   bool mat_pending = false;   // an optimistic decode's byte materialization waits for its confirmation
   struct LastCall {
@@ -206,6 +207,12 @@ int tfrg_ctx_create(int device, tfrg_ctx** out) {
     delete c;
     set_error("hipStreamCreate failed");
     return TFRG_E_HIP;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->info_pin), (kInfoCount + 8) * 4) != hipSuccess) {
+    (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    set_error("hipHostMalloc failed");
+    return TFRG_E_NOMEM;
   }
   // CRC tables: [4][256] slice-by-4 + [4][256] multiply-by-x^8192 (streaming CRC), then
   // [8][256] slice-by-8 (lane kernel), then [16][256] slice-by-16 (streaming CRC), ..., then at
@@ -271,6 +278,7 @@ int tfrg_ctx_destroy(tfrg_ctx* c) {
   if (c->have_events)
     for (auto& e : c->ev) (void)hipEventDestroy(e);
   if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+  if (c->info_pin) (void)hipHostFree(c->info_pin);
   delete c;
   return 0;
 }
@@ -1272,11 +1280,14 @@ int tfrg_decode_host(tfrg_ctx* c, const uint8_t* h_bytes, uint64_t nbytes, const
 // value-capacity hint was too small for it (again with the worst-case capacities).
 static int finish_decode(tfrg_ctx* c, uint32_t* h, uint64_t* kt) {
   bool widened = false;
+  // (into pinned memory, allocated with the context: two DMA copies instead of staged pageable ones)
   for (;;) {
-    HIP_TRY(hipMemcpyAsync(h, c->info.as<uint32_t>() + c->info_slot * kInfoCount, kInfoCount * 4,
+    HIP_TRY(hipMemcpyAsync(c->info_pin, c->info.as<uint32_t>() + c->info_slot * kInfoCount, kInfoCount * 4,
                            hipMemcpyDeviceToHost, c->last_stream));
-    HIP_TRY(hipMemcpyAsync(kt, c->kind_totals.p, 32, hipMemcpyDeviceToHost, c->last_stream));
+    HIP_TRY(hipMemcpyAsync(c->info_pin + kInfoCount, c->kind_totals.p, 32, hipMemcpyDeviceToHost, c->last_stream));
     HIP_TRY(hipStreamSynchronize(c->last_stream));
+    memcpy(h, c->info_pin, kInfoCount * 4);
+    memcpy(kt, c->info_pin + kInfoCount, 32);
     const bool full = c->opt_pending && h[kInfoResid] != 0;  // (records no template took)
     const bool widen = h[kInfoOverflow] && c->hinted && !widened;
     if (!full && !widen) {
