@@ -150,7 +150,9 @@ uint32_t tfrg_masked_crc32c(const uint8_t* p, uint64_t n) { return crc_mask(tfrg
 //   start = ftell; fread(8) != 8 -> stop; fseek(+4) (past EOF is allowed);
 //   push (start, start + 16 + len, len); fseek(+(long)(len + 4)) fails -> stop.
 // A last record whose payload runs past EOF is therefore indexed (verified in the survey).
-int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out, int64_t cap) {
+extern "C++" {
+template <class Put>
+static inline int64_t index_walk(const uint8_t* file, uint64_t size, int64_t cap, Put put) {
   int64_t n = 0, pos = 0;
   for (;;) {
     if ((uint64_t)pos + 8 > size) break;
@@ -158,11 +160,7 @@ int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out, int
     uint64_t length;
     memcpy(&length, file + pos, 8);
     pos += 12;
-    if (n < cap) {
-      out[3 * n] = start;
-      out[3 * n + 1] = start + 16 + length;  // u64 arithmetic, as the reference
-      out[3 * n + 2] = length;
-    }
+    if (n < cap) put(n, start, length);
     ++n;
     const int64_t off = (int64_t)(length + 4);  // fseek's long offset
     int64_t np;
@@ -170,6 +168,25 @@ int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out, int
     pos = np;
   }
   return n;
+}
+}  // extern "C++"
+
+int64_t tfrg_index_buffer(const uint8_t* file, uint64_t size, uint64_t* out, int64_t cap) {
+  return index_walk(file, size, cap, [out](int64_t n, uint64_t start, uint64_t length) {
+    out[3 * n] = start;
+    out[3 * n + 1] = start + 16 + length;  // u64 arithmetic, as the reference
+    out[3 * n + 2] = length;
+  });
+}
+
+// The same walk writing the (start, end) columns of a batch directly, shifted by the piece's offset
+// in the batch (the stream's staging index; internal, not part of the C-ABI).
+int64_t tfrg_index_split(const uint8_t* file, uint64_t size, uint64_t base, uint64_t* starts, uint64_t* ends,
+                         int64_t cap) {
+  return index_walk(file, size, cap, [=](int64_t n, uint64_t start, uint64_t length) {
+    starts[n] = start + base;
+    ends[n] = start + 16 + length + base;
+  });
 }
 
 int tfrg_index_file(const char* path, uint64_t** out_triples, int64_t* n) {

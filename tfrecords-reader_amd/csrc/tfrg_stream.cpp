@@ -26,6 +26,10 @@
 
 #include "../../include/tfrg.h"
 
+// tfrg_host.cpp: the framing walk of tfrg_index_buffer writing split, shifted columns
+extern "C" int64_t tfrg_index_split(const uint8_t* file, uint64_t size, uint64_t base, uint64_t* starts,
+                                    uint64_t* ends, int64_t cap);
+
 namespace tfrg {
 void set_error(const std::string& s);
 }
@@ -178,43 +182,40 @@ static int stage_and_decode(tfrg_stream* s, const Job& j, double* ph) {
     set_error("reading a TFRecord file piece failed");
     return TFRG_E_IO;
   }
-  // framing index of every piece (bit-exact with indexer.pyx:212-252), pieces in parallel, then
-  // shifted to their offsets in the batch
+  // framing index of every piece (bit-exact with indexer.pyx:212-252), pieces in parallel: a count
+  // walk, then a second walk writing each piece's (start, end) columns, shifted to its offset in the
+  // batch, straight into the pinned staging index (both walks touch 8 bytes per record)
   const size_t P = j.pieces.size();
-  std::vector<uint64_t> base(P + 1, 0);
+  std::vector<uint64_t> base(P + 1, 0), cnt(P, 0), first(P + 1, 0);
   for (size_t i = 0; i < P; ++i) base[i + 1] = base[i] + j.pieces[i].size;
-  std::vector<std::vector<uint64_t>> tri(P);
-  {
-    const int T = std::max(1, std::min<int>(s->copy_threads, (int)P));
+  const int T = std::max(1, std::min<int>(s->copy_threads, (int)P));
+  auto run = [&](auto&& body) {
     std::vector<std::thread> ts;
-    auto work = [&](int t) {
-      for (size_t i = t; i < P; i += T) {
-        const int64_t c = tfrg_index_buffer(s->h_buf[k] + base[i], j.pieces[i].size, nullptr, 0);
-        tri[i].resize(3 * (size_t)(c > 0 ? c : 0));
-        if (c > 0) tfrg_index_buffer(s->h_buf[k] + base[i], j.pieces[i].size, tri[i].data(), c);
-      }
-    };
-    for (int t = 1; t < T; ++t) ts.emplace_back(work, t);
-    work(0);
+    for (int q = 1; q < T; ++q) ts.emplace_back(body, q);
+    body(0);
     for (auto& th : ts) th.join();
+  };
+  run([&](int q) {
+    for (size_t i = q; i < P; i += T) {
+      const int64_t c = tfrg_index_buffer(s->h_buf[k] + base[i], j.pieces[i].size, nullptr, 0);
+      cnt[i] = c > 0 ? (uint64_t)c : 0u;
+    }
+  });
+  for (size_t i = 0; i < P; ++i) first[i + 1] = first[i] + cnt[i];
+  const uint64_t n = first[P];
+  if (n > s->max_rec) {
+    set_error("too many records for the stream's staging buffer");
+    return TFRG_E_LIMIT;
   }
-  ph[1] = ms_since(t);
   uint64_t* st = s->h_se[k];
-  uint64_t n = 0;
-  s->piece_recs[k].clear();
-  for (size_t i = 0; i < P; ++i) {
-    const uint64_t c = tri[i].size() / 3;
-    if (n + c > s->max_rec) {
-      set_error("too many records for the stream's staging buffer");
-      return TFRG_E_LIMIT;
-    }
-    for (uint64_t r = 0; r < c; ++r) {
-      st[n + r] = tri[i][3 * r] + base[i];
-      st[s->max_rec + n + r] = tri[i][3 * r + 1] + base[i];
-    }
-    n += c;
-    s->piece_recs[k].push_back(c);
-  }
+  run([&](int q) {
+    for (size_t i = q; i < P; i += T)
+      if (cnt[i])
+        tfrg_index_split(s->h_buf[k] + base[i], j.pieces[i].size, base[i], st + first[i],
+                         st + s->max_rec + first[i], (int64_t)cnt[i]);
+  });
+  s->piece_recs[k].assign(cnt.begin(), cnt.end());
+  ph[1] = ms_since(t);
   memset(s->h_buf[k] + total, 0, 16);  // readable padding past the last record
   const uint64_t pad = (total + 15) & ~15ull;
   if (hipMemcpyAsync(s->d_buf[k], s->h_buf[k], pad + 16, hipMemcpyHostToDevice,
