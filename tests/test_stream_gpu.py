@@ -68,3 +68,55 @@ def test_stream_equals_per_file_decode(files, materialize, devices):
     assert len(got) == len(want) > 4 * 2000
     assert got == want
     assert all(g[2] == 0 and g[3] == 7 for g in got)
+
+
+@pytest.fixture(scope="module")
+def edge_files(tmp_path_factory):
+    """Pieces of zero records and framing edges (indexer.pyx:212-252) packed into one batch: an
+    empty file, a file of empty payloads (zero-length records), one with 5 trailing bytes (fewer
+    than a length field: not a record), single-record files, and regular C1 files between them."""
+    d = tmp_path_factory.mktemp("stream_edges")
+    paths = []
+
+    def add(name, data: bytes):
+        p = d / name
+        p.write_bytes(data)
+        paths.append(str(p))
+
+    add("e0-empty.tfrecord", b"")
+    add("e1-c1.tfrecord", writer.frame_records(synth.c1_payloads(700, offset=3)))
+    add("e2-zero-len.tfrecord", writer.frame_records([b""] * 9))
+    add("e3-trailer.tfrecord", writer.frame_records(synth.c1_payloads(65, offset=900)) + b"\x01\x02\x03\x04\x05")
+    add("e4-empty.tfrecord", b"")
+    for k in range(6):
+        add(f"e5-one{k}.tfrecord", writer.frame_records(synth.c1_payloads(1, offset=2000 + k)))
+    add("e6-c1.tfrecord", writer.frame_records(synth.c1_payloads(1300, offset=5000)))
+    return paths
+
+
+def test_stream_edge_pieces_in_one_batch(edge_files):
+    """Every piece's framing index lands at its offset in the batch's staging columns (the stream's
+    per-piece walks, pieces of zero records among them), equal to the per-file decode."""
+    sd = stream.StreamDecoder(0, batch_bytes=1 << 20, copy_threads=4)
+    try:
+        batches = list(sd.batches(edge_files))
+    finally:
+        sd.close()
+    assert len(batches) == 1 and len(batches[0].pieces) == len(edge_files)
+    assert batches[0].piece_records == [0, 700, 9, 65, 0, 1, 1, 1, 1, 1, 1, 1300]
+    got = _by_record(batches)
+    dec = hip.HipDecoder(0)
+    want = []
+    try:
+        for p in edge_files:
+            sb = shard.read_shard([p])
+            if len(sb) == 0:
+                continue
+            r = dec.decode(sb.buf, sb.starts, sb.ends)
+            for j in range(len(sb)):
+                vals = {key: r.slot_values(s, j) for s, key in enumerate(r.slot_key) if r.order[s, j]}
+                want.append((sb.names[0], j, int(r.status[j]), int(r.verdict[j]), vals))
+    finally:
+        dec.close()
+    assert len(got) == len(want) == 700 + 9 + 65 + 6 + 1300
+    assert got == want
