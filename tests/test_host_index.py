@@ -113,3 +113,34 @@ def test_large_index_matches_oracle():
 
     buf, st, en = synth.framed(synth.c1_payloads(5000) + synth.c3_payloads(20))
     assert np.array_equal(native.index_buffer(buf), O.index(buf.tobytes()))
+
+
+@pytest.mark.parametrize("name", G.FILES + G.EDGE_FILES)
+def test_stream_split_index_matches_reference(name):
+    """The stream reader's staging index (tfrg_index_split, tfrg_stream.cpp: the same framing walk
+    writing shifted start / end columns) equals the reference pointers of every golden file,
+    shifted by an arbitrary piece offset, and stops at its capacity like tfrg_index_buffer."""
+    import ctypes as C
+
+    from tfr_reader import _native as N
+
+    data, meta = G.load_file(name)
+    a = np.frombuffer(data, np.uint8)
+    lib = N.lib()
+    fn = lib.tfrg_index_split
+    fn.restype = C.c_int64
+    fn.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_void_p, C.c_void_p, C.c_int64]
+    ptr = np.array(meta["pointers"], np.uint64).reshape(-1, 3)
+    n = ptr.shape[0]
+    base = 123_456_789
+    st = np.full(n + 1, 7, np.uint64)
+    en = np.full(n + 1, 7, np.uint64)
+    got = fn(a.ctypes.data if a.size else None, a.size, base, st.ctypes.data, en.ctypes.data, n)
+    assert got == n
+    assert st[:n].tolist() == (ptr[:, 0] + np.uint64(base)).tolist()
+    assert en[:n].tolist() == (ptr[:, 1] + np.uint64(base)).tolist()
+    assert int(st[n]) == 7 and int(en[n]) == 7  # nothing written past n
+    if n > 1:  # a short capacity counts every record but writes only `cap` of them
+        st[:] = 0
+        assert fn(a.ctypes.data, a.size, 0, st.ctypes.data, en.ctypes.data, 1) == n
+        assert st[1:].tolist() == [0] * n
